@@ -1,0 +1,248 @@
+"""Python host binding of the batched Paxos C ABI (include/paxos_batch.h).
+
+This is the host side above the C-ABI for environments without GHC (the
+reference's own host is Haskell: /root/reference/app/Main.hs; the Haskell
+binding a maintainer would add lives in hs/ and INTEGRATION.md).  It mirrors
+the reference's vocabulary (/root/reference/src/Common.hs:20-68): ``Ticket``,
+``Command`` ("c<clientId>.<t>", Client.hs:202-203), ``Proposal``,
+``ClientRequest`` / ``ServerResponse`` constructors.
+
+The product path is ``libpaxos_batch.so`` (HIP kernels for gfx950).  There is
+NO CPU fallback here: when the library (or a GPU) is missing every entry point
+raises.  The CPU restatement used as test oracle lives in ``oracle/`` and is
+never imported by this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "csrc", "libpaxos_batch.so")
+
+# ---- constants (include/paxos_batch.h) ------------------------------------
+PXB_OK, PXB_E_INVAL, PXB_E_HIP, PXB_E_OOM, PXB_E_NODEV, PXB_E_RCCL = 0, -1, -2, -3, -4, -5
+MAX_PROPOSERS, MIN_ACCEPTORS, MAX_ACCEPTORS = 3, 2, 9
+MAX_DELAY, MAX_STEP_CAP, QUEUE_DEPTH, LOG_TRACK = 15, 8192, 8, 32
+CFG_RANDOMIZE = 1
+
+F_UNDECIDED, F_STUCK, F_PANIC, F_LOG_DIVERGENCE = 1, 2, 4, 8
+F_STEP_CAP, F_QUEUE_OVERFLOW, F_TICKET_OVERFLOW, F_LOG_TRUNC = 16, 32, 64, 128
+FLAG_NAMES = {F_UNDECIDED: "UNDECIDED", F_STUCK: "STUCK", F_PANIC: "PANIC",
+              F_LOG_DIVERGENCE: "LOG_DIVERGENCE", F_STEP_CAP: "STEP_CAP",
+              F_QUEUE_OVERFLOW: "QUEUE_OVERFLOW", F_TICKET_OVERFLOW: "TICKET_OVERFLOW",
+              F_LOG_TRUNC: "LOG_TRUNC"}
+
+NCOUNTERS = 16
+COUNTER_NAMES = ["decided", "undecided", "stuck", "panic", "divergence", "step_cap",
+                 "rounds", "messages", "queue_overflow", "ticket_overflow", "log_trunc",
+                 "canon_bytes", "steps", "instances", "reserved14", "reserved15"]
+
+# ClientRequest (Common.hs:41-45) / ServerResponse (Common.hs:49-53) tags
+AskForTicket, Propose, Execute = 0, 1, 2
+Round1OK, HaveTicket, Round2Success = 0, 1, 2
+Tick = 3
+MSG_NONE = 0xFFFFFFFF
+Idle, Round1, Round2 = 0, 1, 2
+
+
+class pxb_config(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("first_instance", C.c_uint64),
+                ("n_instances", C.c_uint64), ("n_proposers", C.c_uint32),
+                ("n_acceptors", C.c_uint32), ("loss_ppm", C.c_uint32),
+                ("delay_max", C.c_uint32), ("crash_ppm", C.c_uint32),
+                ("crash_len_max", C.c_uint32), ("crash_start_max", C.c_uint32),
+                ("skew_max", C.c_uint32), ("step_cap", C.c_uint32), ("flags", C.c_uint32)]
+
+
+class pxb_result(C.Structure):
+    _fields_ = [("decided_val", C.c_uint32), ("decided_ticket", C.c_int32),
+                ("rounds", C.c_uint32), ("flags", C.c_uint32)]
+
+
+class pxb_acceptor_rec(C.Structure):
+    _fields_ = [("t_max", C.c_int32), ("t_store", C.c_int32), ("val", C.c_uint32),
+                ("meta", C.c_uint32)]
+
+
+class pxb_counters(C.Structure):
+    _fields_ = [("c", C.c_int64 * NCOUNTERS)]
+
+
+class pxb_msg(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("x", C.c_int32), ("y", C.c_int32), ("z", C.c_uint32)]
+
+
+class pxb_proposer_rec(C.Structure):
+    _fields_ = [("ticket", C.c_int32), ("cmd", C.c_uint32), ("acks", C.c_uint32),
+                ("state", C.c_uint32), ("mr_t", C.c_int32), ("mr_v", C.c_uint32),
+                ("r2_t", C.c_int32), ("r2_v", C.c_uint32), ("pending", C.c_uint32),
+                ("client_id", C.c_uint32)]
+
+
+assert C.sizeof(pxb_config) == 64 and C.sizeof(pxb_result) == 16
+assert C.sizeof(pxb_acceptor_rec) == 16 and C.sizeof(pxb_msg) == 16
+
+# ---- Common.hs vocabulary ------------------------------------------------
+
+
+def command(client_id: int, t: int) -> int:
+    """Encode the Command "c<clientId>.<t>" (Client.hs:202-203)."""
+    return ((client_id & 0xFF) << 24) | (t & 0xFFFFFF)
+
+
+def command_str(code: int) -> Optional[str]:
+    """Decode a Command code back into the reference's String (None = Nothing)."""
+    if code == 0:
+        return None
+    return "c%d.%d" % (code >> 24, code & 0xFFFFFF)
+
+
+def flag_names(flags: int):
+    return [n for b, n in FLAG_NAMES.items() if flags & b]
+
+
+# ---- named configurations (BASELINE.json configs) -------
+@dataclass
+class Config:
+    seed: int
+    n_proposers: int = 1
+    n_acceptors: int = 5
+    loss_ppm: int = 0
+    delay_max: int = 1
+    crash_ppm: int = 0
+    crash_len_max: int = 1
+    crash_start_max: int = 0
+    skew_max: int = 0
+    step_cap: int = 256
+    randomize: bool = False
+
+    def to_c(self, first_instance: int, n_instances: int) -> pxb_config:
+        return pxb_config(self.seed, first_instance, n_instances, self.n_proposers,
+                          self.n_acceptors, self.loss_ppm, self.delay_max, self.crash_ppm,
+                          self.crash_len_max, self.crash_start_max, self.skew_max,
+                          self.step_cap, CFG_RANDOMIZE if self.randomize else 0)
+
+
+CONFIGS = {
+    1: Config(seed=0x5EED0001, n_proposers=1, n_acceptors=3),
+    2: Config(seed=0x5EED0002, n_proposers=1, n_acceptors=5),
+    3: Config(seed=0x5EED0003, n_proposers=2, n_acceptors=5, loss_ppm=100000,
+              delay_max=4, skew_max=3, step_cap=256),
+    4: Config(seed=0x5EED0004, n_proposers=2, n_acceptors=7, delay_max=4,
+              crash_ppm=200000, crash_len_max=16, crash_start_max=8, step_cap=256),
+    5: Config(seed=0x5EED0005, n_proposers=3, n_acceptors=9, loss_ppm=300000,
+              delay_max=8, crash_ppm=200000, crash_len_max=16, crash_start_max=16,
+              skew_max=3, step_cap=512, randomize=True),
+}
+CONFIG_INSTANCES = {1: 1 << 10, 2: 1 << 20, 3: 1 << 24, 4: 1 << 26, 5: 1 << 28}
+
+
+def canonical_bytes_nofault(n_acceptors: int) -> int:
+    """B = 196 N + 160 for a fault-free P = 1 instance."""
+    return 196 * n_acceptors + 160
+
+
+# ---- library loading --------------------------------------------------------
+_lib = None
+
+
+class PaxosError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH):
+    """Load libpaxos_batch.so.  Raises (never falls back) when it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise PaxosError("libpaxos_batch.so not built at %s — run __graft_entry__.build()" % path)
+    lib = C.CDLL(path)
+    vp = C.c_void_p
+    lib.pxb_run.argtypes = [C.POINTER(pxb_config), vp, vp, vp, vp]
+    lib.pxb_run.restype = C.c_int
+    lib.pxb_run_device.argtypes = [C.POINTER(pxb_config), vp, vp, vp, vp, vp]
+    lib.pxb_run_device.restype = C.c_int
+    lib.pxb_acceptor_handle.argtypes = [vp, vp, vp, C.c_uint32]
+    lib.pxb_acceptor_handle.restype = C.c_int
+    lib.pxb_proposer_handle.argtypes = [vp, C.c_uint32, vp, vp, vp, C.c_uint32]
+    lib.pxb_proposer_handle.restype = C.c_int
+    lib.pxb_strerror.argtypes = [C.c_int]
+    lib.pxb_strerror.restype = C.c_char_p
+    lib.pxb_last_hip_error.restype = C.c_int
+    lib.pxb_abi_version.restype = C.c_int
+    lib.pxb_canonical_bytes_nofault.argtypes = [C.c_uint32]
+    lib.pxb_canonical_bytes_nofault.restype = C.c_uint64
+    _lib = lib
+    return lib
+
+
+def check(rc: int):
+    if rc != PXB_OK:
+        lib = load()
+        raise PaxosError("pxb error %d: %s (hip %d)" % (rc, lib.pxb_strerror(rc).decode(),
+                                                         lib.pxb_last_hip_error()))
+
+
+def _ptr(a):
+    """Address of a numpy array / torch tensor / None."""
+    if a is None:
+        return None
+    if hasattr(a, "data_ptr"):
+        return C.c_void_p(a.data_ptr())
+    return C.c_void_p(a.ctypes.data)
+
+
+def run(cfg: Config, first_instance: int, n_instances: int, want_results=True,
+        want_digests=True, want_acceptors=False):
+    """Host-buffer batch run (pxb_run).  Returns numpy arrays + counters dict."""
+    import numpy as np
+    lib = load()
+    N = cfg.n_acceptors
+    res = np.zeros((n_instances, 4), dtype=np.uint32) if want_results else None
+    dig = np.zeros((n_instances, N), dtype=np.uint32) if want_digests else None
+    acc = np.zeros((n_instances, N, 4), dtype=np.uint32) if want_acceptors else None
+    tot = pxb_counters()
+    c = cfg.to_c(first_instance, n_instances)
+    check(lib.pxb_run(C.byref(c), _ptr(res), _ptr(dig), _ptr(acc), C.cast(C.byref(tot), C.c_void_p)))
+    return res, dig, acc, counters_dict(tot.c)
+
+
+def run_device(cfg: Config, first_instance: int, n_instances: int, d_results=None,
+               d_digests=None, d_acceptors=None, d_totals=None, stream=None):
+    """Device-buffer, asynchronous batch run (pxb_run_device) on torch tensors."""
+    lib = load()
+    c = cfg.to_c(first_instance, n_instances)
+    s = C.c_void_p(stream) if stream else None
+    check(lib.pxb_run_device(C.byref(c), _ptr(d_results), _ptr(d_digests), _ptr(d_acceptors),
+                             _ptr(d_totals), s))
+
+
+def counters_dict(c) -> dict:
+    return {COUNTER_NAMES[i]: int(c[i]) for i in range(NCOUNTERS)}
+
+
+def acceptor_handle(states, msgs):
+    """GPU hook: handleClientRequest (Server.hs:51-78) on arrays of
+    pxb_acceptor_rec / pxb_msg (numpy uint32 views, shape (n, 4))."""
+    import numpy as np
+    lib = load()
+    n = len(states)
+    reply = np.zeros((n, 4), dtype=np.uint32)
+    check(lib.pxb_acceptor_handle(_ptr(states), _ptr(msgs), _ptr(reply), n))
+    return reply
+
+
+def proposer_handle(states, n_acceptors, msgs):
+    """GPU hook: handleServerResponse / handleTick (Client.hs:125-207) on
+    arrays of pxb_proposer_rec (uint32 (n,10)) / pxb_msg (uint32 (n,4))."""
+    import numpy as np
+    lib = load()
+    n = len(states)
+    bc = np.zeros((n, 2, 4), dtype=np.uint32)
+    nb = np.zeros(n, dtype=np.uint32)
+    check(lib.pxb_proposer_handle(_ptr(states), n_acceptors, _ptr(msgs), _ptr(bc), _ptr(nb), n))
+    return bc, nb

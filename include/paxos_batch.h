@@ -1,0 +1,179 @@
+/*
+ * paxos_batch.h — C ABI of the MI355X batched single-decree ticket-Paxos engine.
+ *
+ * This is the drop-in boundary for the hot path of rgrover/cloud-haskell-paxos.
+ * The reference has NO FFI of its own: its externally visible
+ * surface is
+ *     server :: Process ()                        /root/reference/src/Server.hs:44
+ *     client :: [ProcessId] -> Int -> Process ()  /root/reference/src/Client.hs:85
+ * spawned N x / P x by  main  (/root/reference/app/Main.hs:41-46), with the
+ * message vocabulary of /root/reference/src/Common.hs:20-68.  A batch driver in
+ * app/Main.hs binds the functions below with `foreign import ccall safe`
+ * (INTEGRATION.md shows the binding).  Each call runs many independent Paxos
+ * instances (N acceptors + P proposers each) under the canonical step schedule
+ * of docs/SEMANTICS.md on the GPU and returns the per-instance outcome.
+ *
+ * Plain C types only.  No C++ exceptions cross this boundary.  All functions
+ * return 0 on success or a negative PXB_E_* code.  Protocol failures (panic,
+ * stuck, divergence, ...) are DATA in pxb_result.flags, not errors.
+ */
+#ifndef PAXOS_BATCH_H
+#define PAXOS_BATCH_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PXB_ABI_VERSION 1
+
+/* ---- error codes ---------------------------------------------------------- */
+#define PXB_OK          0
+#define PXB_E_INVAL    -1   /* bad config / null pointer / out-of-range field  */
+#define PXB_E_HIP      -2   /* HIP runtime error (detail: pxb_last_hip_error)   */
+#define PXB_E_OOM      -3   /* device allocation failed                          */
+#define PXB_E_NODEV    -4   /* no GPU visible                                    */
+#define PXB_E_RCCL     -5   /* collective failure                                */
+
+/* ---- limits of the canonical schedule (docs/SEMANTICS.md §3) ------------ */
+#define PXB_MAX_PROPOSERS   3
+#define PXB_MIN_ACCEPTORS   2
+#define PXB_MAX_ACCEPTORS   9
+#define PXB_MAX_DELAY      15
+#define PXB_MAX_STEP_CAP 8192
+#define PXB_QUEUE_DEPTH     8    /* messages per directed link              */
+#define PXB_LOG_TRACK      32    /* log positions checked for divergence    */
+#define PXB_TICKET_LIMIT (1 << 15)
+
+/* pxb_config.flags */
+#define PXB_CFG_RANDOMIZE 1u     /* config-5 fuzz: per-instance P, loss, delay,
+                                    crash drawn from Philox (n_proposers,
+                                    loss_ppm, delay_max, crash_ppm are maxima) */
+
+/* Everything that defines a batch.  Mirrors the hard-coded constants of the
+ * reference (N = 2 acceptors Main.hs:41, P = 2 proposers Main.hs:45, majority
+ * rule Client.hs:191-194) plus the new fault schedule. */
+typedef struct pxb_config {
+  uint64_t seed;             /* Philox key                                     */
+  uint64_t first_instance;   /* global id of the first instance (sharding)    */
+  uint64_t n_instances;      /* instances in this call                        */
+  uint32_t n_proposers;      /* P: 1..3   (clientId = p+1, Client.hs:85)      */
+  uint32_t n_acceptors;      /* N: 2..9   (length serverPids, Client.hs:193)  */
+  uint32_t loss_ppm;         /* per-message loss probability, ppm             */
+  uint32_t delay_max;        /* link delay uniform in [1, delay_max], 1..15   */
+  uint32_t crash_ppm;        /* per-acceptor isolation-window probability     */
+  uint32_t crash_len_max;    /* window length uniform in [1, crash_len_max]   */
+  uint32_t crash_start_max;  /* window start uniform in [0, crash_start_max]  */
+  uint32_t skew_max;         /* proposer Tick step uniform in [0, skew_max]   */
+  uint32_t step_cap;         /* 1..8192                                        */
+  uint32_t flags;            /* PXB_CFG_*                                      */
+} pxb_config;
+
+/* Per-instance outcome (16 B).  decided_val is the Command of the first
+ * `Execute` broadcast (Client.hs:178) encoded (clientId << 24) | t, i.e.
+ * "c<clientId>.<t>" (Client.hs:202-203); 0 = none.  flags bits 0..7 are the
+ * PXB_F_* bits, bits 16..31 the number of steps the instance ran. */
+typedef struct pxb_result {
+  uint32_t decided_val;
+  int32_t  decided_ticket;   /* Ticket of that Execute (Common.hs:20)          */
+  uint32_t rounds;           /* AskForTicket broadcasts, all proposers         */
+  uint32_t flags;
+} pxb_result;
+
+#define PXB_F_UNDECIDED       (1u << 0)  /* no Execute ever sent               */
+#define PXB_F_STUCK           (1u << 1)  /* quiescent, some proposer not Idle  */
+#define PXB_F_PANIC           (1u << 2)  /* Server.hs:76 pattern failure (Q6)  */
+#define PXB_F_LOG_DIVERGENCE  (1u << 3)  /* two acceptor logs differ           */
+#define PXB_F_STEP_CAP        (1u << 4)
+#define PXB_F_QUEUE_OVERFLOW  (1u << 5)
+#define PXB_F_TICKET_OVERFLOW (1u << 6)
+#define PXB_F_LOG_TRUNC       (1u << 7)  /* a log longer than PXB_LOG_TRACK    */
+#define PXB_RESULT_STEPS(f)   ((f) >> 16)
+
+/* Final acceptor record (16 B) — ServerState, Server.hs:24-31.
+ * meta = log_len | (dead << 31).  val == 0 means `_proposal = Nothing`. */
+typedef struct pxb_acceptor_rec {
+  int32_t  t_max;            /* _largestIssuedTicket */
+  int32_t  t_store;          /* fst of _proposal     */
+  uint32_t val;              /* snd of _proposal     */
+  uint32_t meta;
+} pxb_acceptor_rec;
+
+/* Run totals (SURVEY.md §8(e) slots 0..7, extended). */
+#define PXB_NCOUNTERS 16
+enum {
+  PXB_C_DECIDED = 0, PXB_C_UNDECIDED, PXB_C_STUCK, PXB_C_PANIC,
+  PXB_C_DIVERGENCE, PXB_C_STEP_CAP, PXB_C_ROUNDS, PXB_C_MESSAGES,
+  PXB_C_QUEUE_OVERFLOW, PXB_C_TICKET_OVERFLOW, PXB_C_LOG_TRUNC,
+  PXB_C_CANON_BYTES,         /* SURVEY.md §8(d) canonical accounting v1       */
+  PXB_C_STEPS, PXB_C_INSTANCES, PXB_C_RESERVED14, PXB_C_RESERVED15
+};
+typedef struct pxb_counters { int64_t c[PXB_NCOUNTERS]; } pxb_counters;
+
+/* ---- batch entry points ---------------------------------------------------
+ * pxb_run: HOST buffers.  Runs cfg->n_instances instances on the current HIP
+ * device, copies the outputs back.  out: n_instances results; log_digest:
+ * n_instances * n_acceptors FNV-1a digests (instance-major); acc:
+ * n_instances * n_acceptors final acceptor records; totals: run totals.  Every
+ * output pointer is nullable.  Blocks until done.
+ * Replaces: Main.hs:37-53 (spawn servers/clients, run forever) for a batch.   */
+int pxb_run(const pxb_config* cfg, pxb_result* out, uint32_t* log_digest,
+            pxb_acceptor_rec* acc, pxb_counters* totals);
+
+/* pxb_run_device: DEVICE buffers, asynchronous on `stream` (a hipStream_t;
+ * NULL = default stream).  Same outputs as pxb_run but all pointers are device
+ * pointers on the current device.  d_totals (PXB_NCOUNTERS int64) is ADDED to,
+ * not overwritten, so many launches can accumulate into one vector.         */
+int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_digest,
+                   pxb_acceptor_rec* d_acc, int64_t* d_totals, void* stream);
+
+/* ---- single-handler hooks (run the kernel's own device functions) -------- */
+/* One message in or out.  Requests (ClientRequest, Common.hs:41-45):
+ *   kind 0 AskForTicket t | 1 Propose (t, c) | 2 Execute t ; x = t, z = c.
+ * Responses (ServerResponse, Common.hs:49-53):
+ *   kind 0 Round1OK g (t_store, val) | 1 HaveTicket u | 2 Round2Success ;
+ *   x = g or u, y = t_store, z = val.                                        */
+typedef struct pxb_msg { uint32_t kind; int32_t x; int32_t y; uint32_t z; } pxb_msg;
+#define PXB_MSG_NONE 0xFFFFFFFFu   /* kind of an absent reply */
+
+/* ClientState, Client.hs:58-67 (+ Round1State/Round2State :36-49). */
+typedef struct pxb_proposer_rec {
+  int32_t  ticket;
+  uint32_t cmd;              /* 0 = Nothing          */
+  uint32_t acks;
+  uint32_t state;            /* 0 Idle, 1 Round1, 2 Round2 */
+  int32_t  mr_t;             /* Round1: MostRecent   */
+  uint32_t mr_v;
+  int32_t  r2_t;             /* Round2: _proposal    */
+  uint32_t r2_v;
+  uint32_t pending;          /* Round2: _originalCommandPending */
+  uint32_t client_id;
+} pxb_proposer_rec;
+
+/* handleClientRequest (Server.hs:51-78) applied to count independent
+ * (state, message) pairs on the GPU.  reply[i].kind = PXB_MSG_NONE when the
+ * handler tells nothing.  A panic (Server.hs:76) sets bit 31 of meta.  Host
+ * pointers.                                                                  */
+int pxb_acceptor_handle(pxb_acceptor_rec* states, const pxb_msg* req,
+                        pxb_msg* reply, uint32_t count);
+
+/* handleServerResponse / handleTick (Client.hs:125-207) applied to count
+ * independent (state, message) pairs on the GPU.  msg kind 3 = Tick.  Each
+ * handler broadcasts at most two requests (Client.hs:178,185): bcast[2*i],
+ * bcast[2*i+1], with n_bcast[i] of them valid.  Host pointers.               */
+int pxb_proposer_handle(pxb_proposer_rec* states, uint32_t n_acceptors,
+                        const pxb_msg* msg, pxb_msg* bcast, uint32_t* n_bcast,
+                        uint32_t count);
+
+/* ---- misc ----------------------------------------------------------------- */
+const char* pxb_strerror(int code);
+int         pxb_last_hip_error(void);
+int         pxb_abi_version(void);
+/* canonical algorithmic bytes for a fault-free P = 1 instance */
+uint64_t    pxb_canonical_bytes_nofault(uint32_t n_acceptors);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PAXOS_BATCH_H */
