@@ -1,0 +1,183 @@
+"""Benchmark: Paxos instances decided per second on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2]
+
+One step = one launch of the batched Paxos kernel over one batch of fresh
+synthetic instances (BASELINE config 2 by default: 2^20 instances, 1 proposer,
+5 acceptors, no faults — the single-GPU configuration the metric is quoted
+on).  Instances are generated on the device from (seed, global instance id),
+so the inputs are resident before the timed region; outputs (16 B result +
+4 B/acceptor digest per instance) are written to HBM.  For N > 1 (torchrun,
+one process per GPU) each rank runs its own instance range (weak scaling, no
+data-path collective) and the run counters are summed with one RCCL
+all-reduce.  Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "cloud-haskell-paxos_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import pxb  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
+    ap.add_argument("--instances", type=int, default=0, help="per GPU per step (default: config size, capped)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-extra", action="store_true")
+    return ap.parse_args()
+
+
+def per_gpu_instances(c: int, world: int, override: int) -> int:
+    if override:
+        return override
+    n = pxb.CONFIG_INSTANCES[c]
+    if c == 4:
+        n //= 8                       # config 4 is quoted over 8 GPUs
+    if c == 5:
+        n //= 8
+    return max(1, n // (1 if c in (2, 3) else 1))
+
+
+def run_workload(cfg, n, steps, warmup, rank, world, stream, dev):
+    """Returns (seconds for `steps` timed launches (max over ranks),
+    mean kernel ms, counters dict summed over ranks)."""
+    N = cfg.n_acceptors
+    out = torch.empty((n, 4), dtype=torch.int32, device=dev)
+    dig = torch.empty((n, N), dtype=torch.int32, device=dev)
+    tot = torch.zeros(16, dtype=torch.int64, device=dev)
+    sptr = stream.cuda_stream
+
+    def launch(step):
+        first = (step * world + rank) * n        # fresh global instance ids per step/rank
+        pxb.run_device(cfg, first, n, d_results=out, d_digests=dig, d_totals=tot, stream=sptr)
+
+    with torch.cuda.stream(stream):
+        for w in range(warmup):
+            launch(w)
+        stream.synchronize()
+        tot.zero_()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(steps)]
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(steps):
+            ev[k][0].record(stream)
+            launch(warmup + k)
+            ev[k][1].record(stream)
+        if world > 1:
+            dist.all_reduce(tot)             # RCCL over xGMI: the only collective
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    kms = sum(a.elapsed_time(b) for a, b in ev) / steps
+    return float(elapsed.item()), kms, pxb.counters_dict(tot.cpu().tolist())
+
+
+def cpu_baseline(cfg, budget_s):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_c                          # CPU restatement (oracle/), baseline only
+    threads = min(16, os.cpu_count() or 1)
+    chunk = 1 << 17
+    done, first = 0, 1 << 40
+    t0 = time.perf_counter()
+    while True:
+        oracle_c.run_cpu(cfg, first + done, chunk, threads=threads)
+        done += chunk
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "instances/s", "cores": threads, "kind": "port",
+            "sample": "%d instances of the same config (ids from 2^40), oracle/paxos_oracle.c "
+                      "on %d host threads, %.1f s" % (done, threads, dt)}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    stream = torch.cuda.Stream(dev)
+    c = args.config
+    cfg = pxb.CONFIGS[c]
+    n = per_gpu_instances(c, world, args.instances)
+
+    secs, kms, cnt = run_workload(cfg, n, args.steps, args.warmup, rank, world, stream, dev)
+    total_inst = n * world * args.steps
+    assert cnt["instances"] == total_inst, cnt
+    if c == 2:   # closed forms of the fault-free config: every instance decides
+        assert cnt["decided"] == total_inst and cnt["canon_bytes"] == 1140 * total_inst, cnt
+    value = cnt["decided"] / secs                         # decided instances / s, whole job
+    canon_per_launch = cnt["canon_bytes"] / (args.steps * world)
+    achieved = canon_per_launch / (kms * 1e-3) / 1e9      # GB/s, per-GPU kernel
+    line = {
+        "metric": "Paxos instances decided/sec (node)",
+        "value": value,
+        "unit": "instances/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": secs / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic (Philox4x32-10 schedule from seed + global instance id)",
+        "config": {"workload": "BASELINE config %d" % c, "instances_per_gpu_per_step": n,
+                   "proposers": cfg.n_proposers, "acceptors": cfg.n_acceptors,
+                   "loss_ppm": cfg.loss_ppm, "delay_max": cfg.delay_max, "skew_max": cfg.skew_max,
+                   "crash_ppm": cfg.crash_ppm, "step_cap": cfg.step_cap,
+                   "randomize": cfg.randomize, "seed": hex(cfg.seed),
+                   "parallelism": "instance-range shards x%d" % world},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "accounting": "SURVEY.md 8(d) canonical bytes (%.0f B/instance), "
+                                   "kernel avg %.4f ms/launch (HIP events)" % (
+                                       cnt["canon_bytes"] / max(1, cnt["instances"]), kms)},
+        "counters": cnt,
+    }
+    if rank == 0 and not args.no_extra and c == 2 and world == 1:
+        extra = {}
+        for ec in (3, 5):
+            en = pxb.CONFIG_INSTANCES[ec] if ec == 3 else (1 << 22)
+            es, ek, ecnt = run_workload(pxb.CONFIGS[ec], en, 2, 1, 0, 1, stream, dev)
+            extra["config%d" % ec] = {"instances_per_step": en, "instances_per_s": ecnt["instances"] / es,
+                                      "decided_per_s": ecnt["decided"] / es, "kernel_ms": ek,
+                                      "counters": ecnt}
+        line["extra"] = extra
+    if rank == 0 and world == 1 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

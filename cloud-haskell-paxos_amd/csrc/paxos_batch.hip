@@ -1,0 +1,725 @@
+// paxos_batch.hip — gfx950 batched single-decree ticket-Paxos engine + C ABI.
+//
+// Replaces the reference's per-message actors (Server.hs:44-89 acceptor loop,
+// Client.hs:85-111 proposer loop, spawned by Main.hs:41-46) with one GPU wave
+// per group of independent instances:
+//
+//   * lane = (instance slot g, acceptor a): G = 64 / N instance slots per wave,
+//     lanes g*N .. g*N+N-1 hold the N acceptors of one instance (SoA in VGPRs).
+//   * each acceptor lane owns its directed links: the request queue from every
+//     proposer p (p -> a) and the response queue to every proposer (a -> p),
+//     PXB_QUEUE_DEPTH deep, as register shift-queues with 4-bit due stamps.
+//   * the P proposers of an instance are replicated in all N lanes of its
+//     slot; each response is broadcast to the slot with ds_bpermute and folded
+//     by every lane in canonical (acceptor, link seq) order, so all lanes keep
+//     the same proposer state and each lane enqueues its own copy of a
+//     broadcast on its own link (Philox loss/delay per link, in parallel).
+//   * waves are persistent: when a slot's instance quiesces (or hits
+//     step_cap) the slot writes its outputs and refills from the wave's
+//     contiguous instance range, so divergent instance lengths do not idle
+//     lanes.
+//   * divergence of acceptor logs is detected with LDS compare-and-swap on a
+//     per-slot canonical log (PXB_LOG_TRACK positions).
+//
+// Semantics: docs/SEMANTICS.md; checked bit-exact against oracle/.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <type_traits>
+#include <mutex>
+#include <stdint.h>
+#include <string.h>
+
+#include "../../include/paxos_batch.h"
+#include "paxos_device.h"
+
+namespace pxb {
+
+constexpr int QD = PXB_QUEUE_DEPTH;   // 8: ring slots per directed link
+constexpr int LT = PXB_LOG_TRACK;
+static_assert(QD == 8, "due-nibble word and ring masks assume 8 slots");
+#ifndef PXB_WPB
+#define PXB_WPB 2
+#endif
+constexpr int WPB = PXB_WPB;          // waves per block (LDS is carved per wave)
+constexpr int BLOCK = 64 * WPB;
+#ifndef PXB_OCC_P1
+#define PXB_OCC_P1 4
+#endif
+#ifndef PXB_OCC_P2
+#define PXB_OCC_P2 3
+#endif
+#ifndef PXB_OCC_P3
+#define PXB_OCC_P3 2
+#endif
+
+struct KParams {
+  uint64_t first_instance;
+  uint64_t n_instances;
+  uint64_t loss_thr;                  // precomputed (non-randomized)
+  uint64_t crash_thr;
+  uint32_t k0, k1;
+  uint32_t n_prop, loss_ppm, delay_max, crash_ppm, crash_len_max, crash_start_max;
+  uint32_t skew_max, step_cap, randomize;
+  pxb_result* out;
+  uint32_t* dig;
+  pxb_acceptor_rec* acc;
+  unsigned long long* totals;
+};
+
+__host__ __device__ inline uint64_t prob_threshold(uint32_t ppm) {
+  return ((((uint64_t)ppm) << 32) + 999999ull) / 1000000ull;
+}
+
+// compile-time loop: every per-proposer register index is a constant
+template <int I, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < E) {
+    f(std::integral_constant<int, I>{});
+    static_for<I + 1, E>(f);
+  }
+}
+
+// ---- one directed link = LDS ring (payload) + 3 registers ------------------
+// Tickets never exceed step_cap (<= 8192 < 2^14: a proposer's ticket grows by
+// at most one per step, DESIGN.md "Encodings"), and commands are a clientId
+// (every proposer ticks once, from ticket 0, so t = 1 in "c<id>.1"), so every
+// message is one 32-bit word:
+//   request   x[13:0] | val[15:14] | kind[17:16]
+//   response  x[13:0] | y[27:14]   | val[29:28] | kind[31:30]
+// The due steps (mod 16) of the queued messages sit in one register as a
+// nibble shift-queue, so "how many are due now" needs no LDS access.
+struct Link {
+  uint32_t dn;    // due&15 of entry i in bits [4i+3:4i], entry 0 = head
+  uint32_t hl;    // head[2:0] | len[6:3] | last_due[31:8]
+  uint32_t seq;   // sends attempted on this link (Philox counter word 2)
+};
+__device__ __forceinline__ uint32_t l_len(const Link& L) { return (L.hl >> 3) & 15u; }
+__device__ __forceinline__ uint32_t l_head(const Link& L) { return L.hl & 7u; }
+__device__ __forceinline__ int32_t l_last(const Link& L) { return (int32_t)(L.hl >> 8); }
+// number of entries at the head that are due at step s (due == s <=> nibble == s&15,
+// because every queued due lies in [s, s+15])
+__device__ __forceinline__ uint32_t l_due_count(const Link& L, uint32_t s4) {
+  const uint32_t x = L.dn ^ (s4 * 0x11111111u);
+  const uint32_t tz = x ? (uint32_t)__builtin_ctz(x) : 32u;
+  return min(tz >> 2, l_len(L));
+}
+
+template <int PM, int N>
+struct Lds {
+  static constexpr int G = 64 / N;
+  uint32_t rq[PM][QD][64];       // links p -> a   (lane-interleaved: conflict-free)
+  uint32_t sq[PM][QD][64];       // links a -> p
+  uint32_t clog[G][LT];          // per-slot canonical log (divergence check)
+  uint32_t cnt[PXB_NCOUNTERS];
+};
+
+// occupancy target (waves per SIMD) by proposer count: bounds the VGPR budget
+template <int PM> struct Occ { static constexpr int waves = PXB_OCC_P1; };
+template <> struct Occ<2> { static constexpr int waves = PXB_OCC_P2; };
+template <> struct Occ<3> { static constexpr int waves = PXB_OCC_P3; };
+
+template <int PM, int N>
+__global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KParams kp) {
+  constexpr int G = 64 / N;
+  __shared__ Lds<PM, N> s_lds[WPB];
+
+  const int lane = threadIdx.x & 63;
+  const int wib = threadIdx.x >> 6;
+  Lds<PM, N>& L = s_lds[wib];
+  const int g = lane / N;
+  const int a = lane - g * N;
+  const bool used = g < G;
+  const int base = g * N;
+  const uint64_t gmask = used ? ((((1ull << N) - 1ull)) << base) : 0ull;
+  const uint64_t below = (1ull << base) - 1ull;      // base <= 63
+  uint32_t* clog = &L.clog[used ? g : 0][0];
+  if (lane < PXB_NCOUNTERS) L.cnt[lane] = 0;
+
+  const uint64_t wave = (uint64_t)blockIdx.x * WPB + wib;
+  const uint64_t nwaves = (uint64_t)gridDim.x * WPB;
+  const uint64_t n = kp.n_instances;
+  uint64_t next = n * wave / nwaves;
+  const uint64_t end = n * (wave + 1) / nwaves;
+  const uint32_t k0 = kp.k0, k1 = kp.k1;
+
+  // ---- slot / instance state (slot-uniform unless marked "lane") ----
+  bool active = false;
+  uint64_t idx = 0;
+  uint32_t ilo = 0, ihi = 0;
+  int32_t s = 0;
+  uint32_t P = 0;
+  uint64_t loss_thr = 0;
+  uint32_t delay_max = 1;
+  bool faulty = false;
+  int32_t skew[PM];
+  int32_t last_tick = 0;
+  int32_t c0 = 0, c1 = 0;                 // lane: isolation window of acceptor a
+  AccState A{0, 0, 0, false};             // lane: acceptor a (ServerState)
+  uint32_t log_len = 0, digest = 0;       // lane
+  PropState S[PM];                        // replicated proposers (ClientState)
+  Link R[PM], Sx[PM];                     // lane: links p -> a, a -> p
+  uint32_t lflags = 0;                    // lane-local flag bits
+  uint32_t tflags = 0;                    // replicated flag bits
+  uint32_t rounds = 0, dval = 0;
+  int32_t dtick = 0;
+  bool decided = false;
+  uint32_t msgs_acc = 0;                  // lane totals across instances
+  uint64_t canon_acc = 0;
+#pragma unroll
+  for (int p = 0; p < PM; ++p) {
+    skew[p] = 0;
+    S[p] = PropState{0, 0, 0, IDLE, 0, 0, 0, 0, false};
+    R[p] = Link{0, 0, 0};
+    Sx[p] = Link{0, 0, 0};
+  }
+
+  // common link send (docs/SEMANTICS.md §5): Philox loss/delay, FIFO due,
+  // bounded ring (overflow -> flag, message dropped)
+  auto link_send = [&](Link& Lk, uint32_t* ring, uint32_t dirbits, uint32_t word) {
+    msgs_acc++;
+    const uint32_t k = Lk.seq++;
+    int32_t d = 1;
+    bool ok = true;
+    if (faulty) {
+      const uint4 w = philox(ilo, ihi, k, (1u << 24) | dirbits | (uint32_t)a, k0, k1);
+      ok = (uint64_t)w.x >= loss_thr;
+      d = 1 + (int32_t)mulhi_n(w.y, delay_max);
+    }
+    if (ok) {
+      const uint32_t len = l_len(Lk);
+      if (len >= (uint32_t)QD) {
+        lflags |= PXB_F_QUEUE_OVERFLOW;
+      } else {
+        const int32_t due = max(s + d, l_last(Lk));
+        ring[((l_head(Lk) + len) & 7u) * 64u + (uint32_t)lane] = word;
+        Lk.dn |= ((uint32_t)due & 15u) << (4u * len);
+        Lk.hl = (Lk.hl & 7u) | ((len + 1u) << 3) | ((uint32_t)due << 8);
+      }
+    }
+  };
+  auto link_pop = [&](Link& Lk) {
+    Lk.dn >>= 4;
+    Lk.hl = (Lk.hl & ~0x7Fu) | ((Lk.hl + 1u) & 7u) | ((l_len(Lk) - 1u) << 3);
+  };
+  // proposer p's broadcast copy on link p -> a (sendToAllServers, Client.hs:122-123)
+  auto send_req = [&](auto pc, bool has, uint32_t kind, int32_t x, uint32_t z) {
+    constexpr int p = decltype(pc)::value;
+    if (!has) return;
+    if (kind == ASK) rounds++;
+    if (kind == EXECUTE && !decided) {
+      decided = true;
+      dval = S[p].r2_v;
+      dtick = x;
+    }
+    link_send(R[p], &L.rq[p][0][0], (uint32_t)p << 8,
+              ((uint32_t)x & 0x3FFFu) | (z << 14) | (kind << 16));
+  };
+
+  for (;;) {
+    // ---------------- refill free slots from this wave's range -------------
+    const uint64_t freeb = __ballot(used && !active && a == 0);
+    if (freeb != 0ull && next < end) {
+      const uint64_t cand = next + (uint64_t)__popcll(freeb & below);
+      if (used && !active && cand < end) {
+        idx = cand;
+        const uint64_t inst = kp.first_instance + cand;
+        ilo = (uint32_t)inst;
+        ihi = (uint32_t)(inst >> 32);
+        P = kp.n_prop;
+        uint32_t dmax = kp.delay_max, cppm = kp.crash_ppm;
+        loss_thr = kp.loss_thr;
+        uint64_t crash_thr = kp.crash_thr;
+        if (kp.randomize) {                      // SEMANTICS §4 (config-5 fuzz)
+          const uint4 w = philox(ilo, ihi, 0u, 4u << 24, k0, k1);
+          P = 1u + mulhi_n(w.x, kp.n_prop);
+          loss_thr = prob_threshold(mulhi_n(w.y, kp.loss_ppm + 1u));
+          dmax = 1u + mulhi_n(w.z, kp.delay_max);
+          cppm = mulhi_n(w.w, kp.crash_ppm + 1u);
+          crash_thr = prob_threshold(cppm);
+        }
+        delay_max = dmax;
+        faulty = (loss_thr > 0) || (dmax > 1u);
+        last_tick = 0;
+        uint4 wsk = make_uint4(0, 0, 0, 0);
+        if (kp.skew_max > 0u) wsk = philox(ilo, ihi, 0u, 2u << 24, k0, k1);
+        static_for<0, PM>([&](auto pc) {
+          constexpr int p = decltype(pc)::value;
+          const uint32_t wp = (p == 0) ? wsk.x : (p == 1) ? wsk.y : wsk.z;
+          skew[p] = (kp.skew_max > 0u) ? (int32_t)mulhi_n(wp, kp.skew_max + 1u) : 0;
+          if ((uint32_t)p < P) last_tick = max(last_tick, skew[p]);
+          S[p] = PropState{0, 0, 0, IDLE, 0, 0, 0, 0, false};
+          R[p] = Link{0, 0, 0};
+          Sx[p] = Link{0, 0, 0};
+        });
+        c0 = c1 = 0;
+        if (cppm > 0u) {
+          const uint4 w = philox(ilo, ihi, 0u, (3u << 24) | (uint32_t)a, k0, k1);
+          if ((uint64_t)w.x < crash_thr) {
+            c0 = (int32_t)mulhi_n(w.y, kp.crash_start_max + 1u);
+            c1 = c0 + 1 + (int32_t)mulhi_n(w.z, kp.crash_len_max);
+          }
+        }
+        A = AccState{0, 0, 0, false};
+        log_len = 0;
+        digest = 0x811C9DC5u;
+        lflags = tflags = 0;
+        rounds = dval = 0;
+        dtick = 0;
+        decided = false;
+        s = 0;
+        for (int k = a; k < LT; k += N) clog[k] = 0u;
+        active = true;
+      }
+      next = min(next + (uint64_t)__popcll(freeb), end);
+    }
+    if (!__any(active)) break;
+
+    const uint32_t s4 = (uint32_t)s & 15u;
+    // ---------------- acceptor phase: (proposer index, link seq) order -------
+    // handleClientRequest, Server.hs:51-78, for every due request of lane a
+    {
+      const bool iso = (c0 <= s) && (s < c1);
+      static_for<0, PM>([&](auto pc) {
+        constexpr int p = decltype(pc)::value;
+        for (;;) {
+          const bool due = active && l_len(R[p]) > 0u && (R[p].dn & 15u) == s4;
+          if (!__any(due)) break;
+          if (due) {
+            const uint32_t w = L.rq[p][l_head(R[p])][lane];
+            link_pop(R[p]);
+            const uint32_t kind = (w >> 16) & 3u;
+            const uint32_t rb = (kind == PROPOSE) ? 12u : 8u;
+            if (A.dead || iso) {
+              canon_acc += rb;                         // written, discarded
+            } else {
+              canon_acc += 2u * rb + 32u;
+              int32_t rx, ry;
+              uint32_t rz, ev;
+              const uint32_t rk = acceptor_step(A, kind, (int32_t)(w & 0x3FFFu), (w >> 14) & 3u,
+                                                rx, ry, rz, ev);
+              if (A.dead) lflags |= PXB_F_PANIC;
+              if (ev != 0u) {
+                digest = fnv_u32(digest, (ev << 24) | 1u);
+                if (log_len < (uint32_t)LT) {
+                  const uint32_t old = atomicCAS(&clog[log_len], 0u, ev);
+                  if (old != 0u && old != ev) lflags |= PXB_F_LOG_DIVERGENCE;
+                } else {
+                  lflags |= PXB_F_LOG_TRUNC;
+                }
+                log_len++;
+              }
+              if (rk != NONE)
+                link_send(Sx[p], &L.sq[p][0][0], (1u << 16) | ((uint32_t)p << 8),
+                          ((uint32_t)rx & 0x3FFFu) | (((uint32_t)ry & 0x3FFFu) << 14) | (rz << 28) | (rk << 30));
+            }
+          }
+        }
+      });
+    }
+
+    // ---------------- proposer phase: Tick, then (acceptor, link seq) order --
+    static_for<0, PM>([&](auto pc) {
+      constexpr int p = decltype(pc)::value;
+      const bool pact = active && (uint32_t)p < P;
+      bool stepped = false;
+      const bool tick = pact && s == skew[p];
+      if (__any(tick)) {                          // handleTick, Client.hs:196-207
+        Req o0{NONE, 0, 0};
+        uint32_t no = 0;
+        if (tick) {
+          no = proposer_tick(S[p], (uint32_t)(p + 1), o0);   // compact cmd = clientId
+          stepped = true;
+        }
+        send_req(pc, no > 0u, o0.kind, o0.x, o0.z);
+      }
+      const uint32_t cnt_p = pact ? l_due_count(Sx[p], s4) : 0u;
+      const uint64_t anyb = __ballot(cnt_p > 0u);
+      if (anyb != 0ull) {
+        stepped = stepped || ((anyb & gmask) != 0ull);
+        // Serial fold in canonical order (acceptor aa, then link seq): every
+        // lane of the slot reads the head of lane aa's link (ds_bpermute) and
+        // applies handleServerResponse (Client.hs:125-189); lane aa pops it.
+#pragma unroll 1
+        for (int aa = 0; aa < N; ++aa) {
+          uint32_t ca = (uint32_t)__shfl((int)cnt_p, base + aa);
+          while (__any(ca > 0u)) {
+            const bool take = ca > 0u;
+            const uint32_t mine = L.sq[p][l_head(Sx[p])][lane];
+            const uint32_t w = (uint32_t)__shfl((int)mine, base + aa);
+            Req o0{NONE, 0, 0}, o1{NONE, 0, 0};
+            uint32_t no = 0;
+            if (take) {
+              const uint32_t kind = w >> 30;
+              no = proposer_step(S[p], (uint32_t)N, kind, (int32_t)(w & 0x3FFFu),
+                                 (int32_t)((w >> 14) & 0x3FFFu), (w >> 28) & 3u, o0, o1);
+              if (a == aa) {
+                canon_acc += 2u * (16u >> kind);
+                link_pop(Sx[p]);
+              }
+              ca--;
+            }
+#pragma unroll 1
+            for (uint32_t k = 0; k < 2u; ++k) {
+              const bool has = no > k;
+              if (__any(has)) {
+                const uint32_t kk = k ? o1.kind : o0.kind;
+                const int32_t kx = k ? o1.x : o0.x;
+                const uint32_t kz = k ? o1.z : o0.z;
+                send_req(pc, has, kk, kx, kz);
+              }
+            }
+          }
+        }
+      }
+      if (stepped && a == 0) canon_acc += 48u;
+      if (pact && S[p].ticket >= PXB_TICKET_LIMIT) tflags |= PXB_F_TICKET_OVERFLOW;
+    });
+
+    // ---------------- end of step: quiescence / step cap ---------------------
+    bool busy = false;
+#pragma unroll
+    for (int p = 0; p < PM; ++p) busy = busy || ((R[p].hl | Sx[p].hl) & 0x78u) != 0u;
+    const uint64_t busyb = __ballot(active && busy);
+    const uint64_t pan = __ballot((lflags & PXB_F_PANIC) != 0u);
+    const uint64_t dvg = __ballot((lflags & PXB_F_LOG_DIVERGENCE) != 0u);
+    const uint64_t qov = __ballot((lflags & PXB_F_QUEUE_OVERFLOW) != 0u);
+    const uint64_t trc = __ballot((lflags & PXB_F_LOG_TRUNC) != 0u);
+    if (active) {
+      const bool quiet = ((busyb & gmask) == 0ull) && s >= last_tick;
+      const bool cap = !quiet && (s + 1 >= (int32_t)kp.step_cap);
+      s++;
+      if (quiet || cap) {
+        uint32_t f = tflags;
+        if (pan & gmask) f |= PXB_F_PANIC;
+        if (dvg & gmask) f |= PXB_F_LOG_DIVERGENCE;
+        if (qov & gmask) f |= PXB_F_QUEUE_OVERFLOW;
+        if (trc & gmask) f |= PXB_F_LOG_TRUNC;
+        if (cap) f |= PXB_F_STEP_CAP;
+        if (!decided) f |= PXB_F_UNDECIDED;
+        if (!cap) {
+#pragma unroll
+          for (int p = 0; p < PM; ++p)
+            if ((uint32_t)p < P && S[p].rs != IDLE) f |= PXB_F_STUCK;
+        }
+        const uint32_t steps = (uint32_t)s;
+        if (a == 0) {
+          if (kp.out) {
+            uint4 r;
+            r.x = decided ? ((dval << 24) | 1u) : 0u;
+            r.y = decided ? (uint32_t)dtick : 0u;
+            r.z = rounds;
+            r.w = (f & 0xFFu) | (min(steps, 0xFFFFu) << 16);
+            *reinterpret_cast<uint4*>(kp.out + idx) = r;
+          }
+          uint32_t* cnt = L.cnt;
+          atomicAdd(&cnt[PXB_C_DECIDED], decided ? 1u : 0u);
+          atomicAdd(&cnt[PXB_C_UNDECIDED], decided ? 0u : 1u);
+          if (f & PXB_F_STUCK) atomicAdd(&cnt[PXB_C_STUCK], 1u);
+          if (f & PXB_F_PANIC) atomicAdd(&cnt[PXB_C_PANIC], 1u);
+          if (f & PXB_F_LOG_DIVERGENCE) atomicAdd(&cnt[PXB_C_DIVERGENCE], 1u);
+          if (f & PXB_F_STEP_CAP) atomicAdd(&cnt[PXB_C_STEP_CAP], 1u);
+          if (f & PXB_F_QUEUE_OVERFLOW) atomicAdd(&cnt[PXB_C_QUEUE_OVERFLOW], 1u);
+          if (f & PXB_F_TICKET_OVERFLOW) atomicAdd(&cnt[PXB_C_TICKET_OVERFLOW], 1u);
+          if (f & PXB_F_LOG_TRUNC) atomicAdd(&cnt[PXB_C_LOG_TRUNC], 1u);
+          atomicAdd(&cnt[PXB_C_ROUNDS], rounds);
+          atomicAdd(&cnt[PXB_C_STEPS], steps);
+          atomicAdd(&cnt[PXB_C_INSTANCES], 1u);
+          canon_acc += 16u;
+        }
+        canon_acc += 4u;
+        if (kp.dig) kp.dig[idx * N + a] = fnv_u32(digest, log_len);
+        if (kp.acc) {
+          uint4 r;
+          r.x = (uint32_t)A.t_max;
+          r.y = (uint32_t)A.t_store;
+          r.z = A.val ? ((A.val << 24) | 1u) : 0u;
+          r.w = log_len | ((A.dead ? 1u : 0u) << 31);
+          *reinterpret_cast<uint4*>(kp.acc + idx * N + a) = r;
+        }
+        active = false;
+      }
+    }
+  }
+
+  // ---------------- flush wave totals -----------------------------------------
+  uint32_t m = msgs_acc;
+  uint64_t c64 = canon_acc;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    m += (uint32_t)__shfl_xor((int)m, off);
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)c64, off);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(c64 >> 32), off);
+    c64 += ((uint64_t)hi << 32) | lo;
+  }
+  if (lane == 0) {
+    atomicAdd(&kp.totals[PXB_C_MESSAGES], (unsigned long long)m);
+    atomicAdd(&kp.totals[PXB_C_CANON_BYTES], (unsigned long long)c64);
+  }
+  if (lane < PXB_NCOUNTERS && lane != PXB_C_MESSAGES && lane != PXB_C_CANON_BYTES) {
+    const uint32_t v = L.cnt[lane];
+    if (v) atomicAdd(&kp.totals[lane], (unsigned long long)v);
+  }
+}
+
+// ---- single-handler hook kernels ------------------------------------------
+__global__ void acceptor_hook_kernel(pxb_acceptor_rec* st, const pxb_msg* in, pxb_msg* out, uint32_t count) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  AccState A{st[i].t_max, st[i].t_store, st[i].val, (st[i].meta >> 31) != 0u};
+  uint32_t log_len = st[i].meta & 0x7FFFFFFFu;
+  pxb_msg r{NONE, 0, 0, 0};
+  if (!A.dead) {
+    int32_t rx, ry;
+    uint32_t rz, ev;
+    const uint32_t rk = acceptor_step(A, in[i].kind, in[i].x, in[i].z, rx, ry, rz, ev);
+    if (ev) log_len++;
+    if (rk != NONE) r = pxb_msg{rk, rx, ry, rz};
+  }
+  st[i] = pxb_acceptor_rec{A.t_max, A.t_store, A.val, log_len | ((A.dead ? 1u : 0u) << 31)};
+  out[i] = r;
+}
+
+__global__ void proposer_hook_kernel(pxb_proposer_rec* st, uint32_t n_acc, const pxb_msg* in,
+                                     pxb_msg* bc, uint32_t* nb, uint32_t count) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  pxb_proposer_rec R = st[i];
+  PropState S{R.ticket, R.cmd, R.acks, R.state, R.mr_t, R.mr_v, R.r2_t, R.r2_v, R.pending != 0u};
+  Req o0{NONE, 0, 0}, o1{NONE, 0, 0};
+  uint32_t no;
+  if (in[i].kind == 3u)
+    no = proposer_tick(S, (R.client_id << 24) | ((uint32_t)(S.ticket + 1) & 0xFFFFFFu), o0);
+  else
+    no = proposer_step(S, n_acc, in[i].kind, in[i].x, in[i].y, in[i].z, o0, o1);
+  st[i] = pxb_proposer_rec{S.ticket, S.cmd, S.acks, S.rs, S.mr_t, S.mr_v, S.r2_t, S.r2_v,
+                           S.pending ? 1u : 0u, R.client_id};
+  bc[2 * i] = (no > 0) ? pxb_msg{o0.kind, o0.x, 0, o0.z} : pxb_msg{NONE, 0, 0, 0};
+  bc[2 * i + 1] = (no > 1) ? pxb_msg{o1.kind, o1.x, 0, o1.z} : pxb_msg{NONE, 0, 0, 0};
+  nb[i] = no;
+}
+
+// ---- host side ----------------------------------------------------------------
+typedef void (*kernel_fn)(KParams);
+
+template <int PM, int N>
+static kernel_fn kfn() { return paxos_batch_kernel<PM, N>; }
+
+template <int PM>
+static kernel_fn pick_n(uint32_t n) {
+  switch (n) {
+    case 2: return kfn<PM, 2>();
+    case 3: return kfn<PM, 3>();
+    case 4: return kfn<PM, 4>();
+    case 5: return kfn<PM, 5>();
+    case 6: return kfn<PM, 6>();
+    case 7: return kfn<PM, 7>();
+    case 8: return kfn<PM, 8>();
+    case 9: return kfn<PM, 9>();
+  }
+  return nullptr;
+}
+
+static kernel_fn pick(uint32_t pm, uint32_t n) {
+  switch (pm) {
+    case 1: return pick_n<1>(n);
+    case 2: return pick_n<2>(n);
+    case 3: return pick_n<3>(n);
+  }
+  return nullptr;
+}
+
+static thread_local int g_last_hip = 0;
+static std::mutex g_mu;
+static int g_occ[4][10][64];            // [pm][n][device] blocks per CU (0 = unknown)
+static int g_cus[64];
+
+static int hip_fail(hipError_t e) {
+  g_last_hip = (int)e;
+  return (e == hipErrorOutOfMemory) ? PXB_E_OOM : PXB_E_HIP;
+}
+#define HIPCHK(x)                                   \
+  do {                                              \
+    hipError_t _e = (x);                            \
+    if (_e != hipSuccess) return hip_fail(_e);      \
+  } while (0)
+
+static int validate(const pxb_config* c) {
+  if (!c) return PXB_E_INVAL;
+  if (c->n_proposers < 1 || c->n_proposers > PXB_MAX_PROPOSERS) return PXB_E_INVAL;
+  if (c->n_acceptors < PXB_MIN_ACCEPTORS || c->n_acceptors > PXB_MAX_ACCEPTORS) return PXB_E_INVAL;
+  if (c->loss_ppm > 1000000u || c->crash_ppm > 1000000u) return PXB_E_INVAL;
+  if (c->delay_max < 1 || c->delay_max > PXB_MAX_DELAY) return PXB_E_INVAL;
+  if (c->crash_len_max < 1 || c->crash_len_max > 4096 || c->crash_start_max > 65535) return PXB_E_INVAL;
+  if (c->skew_max > 4096) return PXB_E_INVAL;
+  if (c->step_cap < 1 || c->step_cap > PXB_MAX_STEP_CAP) return PXB_E_INVAL;
+  if (c->n_instances > (1ull << 40)) return PXB_E_INVAL;
+  return PXB_OK;
+}
+
+}  // namespace pxb
+
+using namespace pxb;
+
+extern "C" {
+
+int pxb_abi_version(void) { return PXB_ABI_VERSION; }
+int pxb_last_hip_error(void) { return g_last_hip; }
+
+const char* pxb_strerror(int code) {
+  switch (code) {
+    case PXB_OK: return "ok";
+    case PXB_E_INVAL: return "invalid argument";
+    case PXB_E_HIP: return "HIP runtime error";
+    case PXB_E_OOM: return "device out of memory";
+    case PXB_E_NODEV: return "no GPU device";
+    case PXB_E_RCCL: return "collective failure";
+  }
+  return "unknown error";
+}
+
+uint64_t pxb_canonical_bytes_nofault(uint32_t n_acceptors) { return 196ull * n_acceptors + 160ull; }
+
+int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_digest,
+                   pxb_acceptor_rec* d_acc, int64_t* d_totals, void* stream) {
+  int rc = validate(cfg);
+  if (rc) return rc;
+  if (!d_totals) return PXB_E_INVAL;
+  if (cfg->n_instances == 0) return PXB_OK;
+  int dev = 0;
+  HIPCHK(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 64) return PXB_E_NODEV;
+  kernel_fn fn = pick(cfg->n_proposers, cfg->n_acceptors);
+  if (!fn) return PXB_E_INVAL;
+  int occ, cus;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_cus[dev]) {
+      hipDeviceProp_t prop;
+      HIPCHK(hipGetDeviceProperties(&prop, dev));
+      g_cus[dev] = prop.multiProcessorCount;
+    }
+    int& o = g_occ[cfg->n_proposers][cfg->n_acceptors][dev];
+    if (!o) {
+      int nb = 0;
+      HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)fn, BLOCK, 0));
+      o = std::max(1, nb);
+    }
+    occ = o;
+    cus = g_cus[dev];
+  }
+  KParams kp;
+  memset(&kp, 0, sizeof(kp));
+  kp.first_instance = cfg->first_instance;
+  kp.n_instances = cfg->n_instances;
+  kp.k0 = (uint32_t)cfg->seed;
+  kp.k1 = (uint32_t)(cfg->seed >> 32);
+  kp.n_prop = cfg->n_proposers;
+  kp.loss_ppm = cfg->loss_ppm;
+  kp.delay_max = cfg->delay_max;
+  kp.crash_ppm = cfg->crash_ppm;
+  kp.crash_len_max = cfg->crash_len_max;
+  kp.crash_start_max = cfg->crash_start_max;
+  kp.skew_max = cfg->skew_max;
+  kp.step_cap = cfg->step_cap;
+  kp.randomize = (cfg->flags & PXB_CFG_RANDOMIZE) ? 1u : 0u;
+  kp.loss_thr = prob_threshold(cfg->loss_ppm);
+  kp.crash_thr = prob_threshold(cfg->crash_ppm);
+  kp.out = d_out;
+  kp.dig = d_log_digest;
+  kp.acc = d_acc;
+  kp.totals = reinterpret_cast<unsigned long long*>(d_totals);
+  const uint64_t G = 64 / cfg->n_acceptors;
+  const uint64_t waves_needed = (cfg->n_instances + G - 1) / G;
+  const uint64_t blocks_needed = (waves_needed + WPB - 1) / WPB;
+  const uint64_t resident = (uint64_t)occ * (uint64_t)cus;
+  const unsigned grid = (unsigned)std::min<uint64_t>(blocks_needed, resident);
+  hipLaunchKernelGGL(fn, dim3(grid), dim3(BLOCK), 0, (hipStream_t)stream, kp);
+  HIPCHK(hipGetLastError());
+  return PXB_OK;
+}
+
+int pxb_run(const pxb_config* cfg, pxb_result* out, uint32_t* log_digest, pxb_acceptor_rec* acc,
+            pxb_counters* totals) {
+  int rc = validate(cfg);
+  if (rc) return rc;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return PXB_E_NODEV;
+  const uint64_t n = cfg->n_instances, N = cfg->n_acceptors;
+  pxb_result* d_out = nullptr;
+  uint32_t* d_dig = nullptr;
+  pxb_acceptor_rec* d_acc = nullptr;
+  int64_t* d_tot = nullptr;
+  hipError_t e = hipSuccess;
+  rc = PXB_OK;
+  do {
+    if (out && n && (e = hipMalloc(&d_out, n * sizeof(pxb_result))) != hipSuccess) break;
+    if (log_digest && n && (e = hipMalloc(&d_dig, n * N * sizeof(uint32_t))) != hipSuccess) break;
+    if (acc && n && (e = hipMalloc(&d_acc, n * N * sizeof(pxb_acceptor_rec))) != hipSuccess) break;
+    if ((e = hipMalloc(&d_tot, PXB_NCOUNTERS * sizeof(int64_t))) != hipSuccess) break;
+    if ((e = hipMemset(d_tot, 0, PXB_NCOUNTERS * sizeof(int64_t))) != hipSuccess) break;
+    rc = pxb_run_device(cfg, d_out, d_dig, d_acc, d_tot, nullptr);
+    if (rc) break;
+    if ((e = hipDeviceSynchronize()) != hipSuccess) break;
+    if (out && n && (e = hipMemcpy(out, d_out, n * sizeof(pxb_result), hipMemcpyDeviceToHost)) != hipSuccess) break;
+    if (log_digest && n &&
+        (e = hipMemcpy(log_digest, d_dig, n * N * sizeof(uint32_t), hipMemcpyDeviceToHost)) != hipSuccess) break;
+    if (acc && n && (e = hipMemcpy(acc, d_acc, n * N * sizeof(pxb_acceptor_rec), hipMemcpyDeviceToHost)) != hipSuccess)
+      break;
+    if (totals && (e = hipMemcpy(totals->c, d_tot, PXB_NCOUNTERS * sizeof(int64_t), hipMemcpyDeviceToHost)) != hipSuccess)
+      break;
+  } while (0);
+  if (e != hipSuccess) rc = hip_fail(e);
+  if (d_out) (void)hipFree(d_out);
+  if (d_dig) (void)hipFree(d_dig);
+  if (d_acc) (void)hipFree(d_acc);
+  if (d_tot) (void)hipFree(d_tot);
+  return rc;
+}
+
+static int run_hook(bool acceptor, void* st, size_t st_bytes, uint32_t n_acc, const pxb_msg* in, pxb_msg* out,
+                    size_t out_n, uint32_t* nb, uint32_t count) {
+  if (!st || !in || !out || (!acceptor && !nb)) return PXB_E_INVAL;
+  if (count == 0) return PXB_OK;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return PXB_E_NODEV;
+  void *d_st = nullptr, *d_in = nullptr, *d_out = nullptr, *d_nb = nullptr;
+  hipError_t e = hipSuccess;
+  do {
+    if ((e = hipMalloc(&d_st, st_bytes * count)) != hipSuccess) break;
+    if ((e = hipMalloc(&d_in, sizeof(pxb_msg) * count)) != hipSuccess) break;
+    if ((e = hipMalloc(&d_out, sizeof(pxb_msg) * out_n * count)) != hipSuccess) break;
+    if (!acceptor && (e = hipMalloc(&d_nb, sizeof(uint32_t) * count)) != hipSuccess) break;
+    if ((e = hipMemcpy(d_st, st, st_bytes * count, hipMemcpyHostToDevice)) != hipSuccess) break;
+    if ((e = hipMemcpy(d_in, in, sizeof(pxb_msg) * count, hipMemcpyHostToDevice)) != hipSuccess) break;
+    const unsigned grid = (count + 255) / 256;
+    if (acceptor)
+      hipLaunchKernelGGL(acceptor_hook_kernel, dim3(grid), dim3(256), 0, 0, (pxb_acceptor_rec*)d_st,
+                         (const pxb_msg*)d_in, (pxb_msg*)d_out, count);
+    else
+      hipLaunchKernelGGL(proposer_hook_kernel, dim3(grid), dim3(256), 0, 0, (pxb_proposer_rec*)d_st, n_acc,
+                         (const pxb_msg*)d_in, (pxb_msg*)d_out, (uint32_t*)d_nb, count);
+    if ((e = hipGetLastError()) != hipSuccess) break;
+    if ((e = hipDeviceSynchronize()) != hipSuccess) break;
+    if ((e = hipMemcpy(st, d_st, st_bytes * count, hipMemcpyDeviceToHost)) != hipSuccess) break;
+    if ((e = hipMemcpy(out, d_out, sizeof(pxb_msg) * out_n * count, hipMemcpyDeviceToHost)) != hipSuccess) break;
+    if (!acceptor && (e = hipMemcpy(nb, d_nb, sizeof(uint32_t) * count, hipMemcpyDeviceToHost)) != hipSuccess) break;
+  } while (0);
+  if (d_st) (void)hipFree(d_st);
+  if (d_in) (void)hipFree(d_in);
+  if (d_out) (void)hipFree(d_out);
+  if (d_nb) (void)hipFree(d_nb);
+  return (e == hipSuccess) ? PXB_OK : hip_fail(e);
+}
+
+int pxb_acceptor_handle(pxb_acceptor_rec* states, const pxb_msg* req, pxb_msg* reply, uint32_t count) {
+  return run_hook(true, states, sizeof(pxb_acceptor_rec), 0, req, reply, 1, nullptr, count);
+}
+
+int pxb_proposer_handle(pxb_proposer_rec* states, uint32_t n_acceptors, const pxb_msg* msg, pxb_msg* bcast,
+                        uint32_t* n_bcast, uint32_t count) {
+  if (n_acceptors < PXB_MIN_ACCEPTORS || n_acceptors > PXB_MAX_ACCEPTORS) return PXB_E_INVAL;
+  return run_hook(false, states, sizeof(pxb_proposer_rec), n_acceptors, msg, bcast, 2, n_bcast, count);
+}
+
+}  // extern "C"

@@ -24,7 +24,7 @@ plus two drivers:
 Parity status: the reference is Haskell (GHC 8.4 / stack lts-12.18) and
 cannot be built or run in this image (no ghc/stack/cabal, no network;
 SURVEY.md §8c).  The restatement is pinned by the hand-derived KATs of
-SURVEY.md §8.0 (tests/test_oracle_kat.py) and the Random123 Philox4x32-10
+SURVEY.md §8.0 (tests/test_oracle.py) and the Random123 Philox4x32-10
 known-answer vectors; it is NOT pinned by executions of the reference itself.
 """
 from __future__ import annotations
@@ -214,7 +214,7 @@ def proposer_tick(pr: Proposer) -> List[Tuple[int, int, int]]:
     return [(ASK, t, NOTHING)]                    # Client.hs:207
 
 
-def proposer_handle(pr: Proposer, n_acceptors: int, kind: int, a: int, b: int = 0,
+def proposer_handle(pr: Proposer, n_acceptors: int, kind: int, a: int = 0, b: int = 0,
                     c: int = NOTHING) -> List[Tuple[int, int, int]]:
     """handleServerResponse (Client.hs:125-189). The sender pid is ignored
     (Client.hs:128,142,172 bind sPid, never used — Q3).  Returns the list of

@@ -1,0 +1,81 @@
+"""CPU-side checks of the C-ABI boundary (include/paxos_batch.h): the HIP
+library loads without a GPU, exports every declared entry point, its structs
+match the header, and it fails loudly (never falls back to a CPU path)."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+import pxb
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "paxos_batch.h")
+
+
+def _declared():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\*?\s+\*?(pxb_[a-z_]+)\s*\(", txt, re.M)))
+
+
+def test_header_declares_the_boundary():
+    names = _declared()
+    for f in ("pxb_run", "pxb_run_device", "pxb_acceptor_handle", "pxb_proposer_handle",
+              "pxb_strerror", "pxb_last_hip_error", "pxb_abi_version"):
+        assert f in names
+
+
+def test_library_exports_every_declared_symbol():
+    lib = pxb.load()
+    out = subprocess.run(["nm", "-D", "--defined-only", pxb.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r" T (pxb_\w+)", out))
+    for name in _declared():
+        assert name in exported, name
+        assert hasattr(lib, name)
+
+
+def test_struct_layout_matches_header():
+    src = r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "paxos_batch.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(pxb_config), sizeof(pxb_result),
+         sizeof(pxb_acceptor_rec), sizeof(pxb_counters), sizeof(pxb_msg), sizeof(pxb_proposer_rec),
+         offsetof(pxb_config, step_cap));
+  return 0;
+}'''
+    tmp = "/tmp/pxb_layout"
+    with open(tmp + ".c", "w") as f:
+        f.write(src)
+    subprocess.run(["gcc", "-I", os.path.dirname(HEADER), "-o", tmp, tmp + ".c"], check=True)
+    got = [int(x) for x in subprocess.run([tmp], capture_output=True, text=True).stdout.split()]
+    assert got == [C.sizeof(pxb.pxb_config), C.sizeof(pxb.pxb_result), C.sizeof(pxb.pxb_acceptor_rec),
+                   C.sizeof(pxb.pxb_counters), C.sizeof(pxb.pxb_msg), C.sizeof(pxb.pxb_proposer_rec),
+                   pxb.pxb_config.step_cap.offset]
+
+
+def test_misc_entry_points_without_gpu():
+    lib = pxb.load()
+    assert lib.pxb_abi_version() == 1
+    assert lib.pxb_strerror(pxb.PXB_E_INVAL) == b"invalid argument"
+    assert lib.pxb_canonical_bytes_nofault(5) == 1140
+
+
+def test_invalid_config_rejected():
+    lib = pxb.load()
+    bad = pxb.Config(seed=1, n_proposers=4).to_c(0, 10)
+    tot = (C.c_int64 * 16)()
+    assert lib.pxb_run_device(C.byref(bad), None, None, None, C.cast(tot, C.c_void_p), None) == pxb.PXB_E_INVAL
+    bad = pxb.Config(seed=1, delay_max=16).to_c(0, 10)
+    assert lib.pxb_run_device(C.byref(bad), None, None, None, C.cast(tot, C.c_void_p), None) == pxb.PXB_E_INVAL
+
+
+def test_no_cpu_fallback_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(pxb.PaxosError):
+        pxb.run(pxb.CONFIGS[2], 0, 16)

@@ -1,0 +1,186 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle,
+bit-exact on results, per-acceptor log digests, final acceptor records and
+run counters; plus size-independent properties at BASELINE.json sizes."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_c
+import pxb
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+THREADS = min(16, os.cpu_count() or 1)
+
+
+def _cmp(cfg, first, n, want_acc=True):
+    res, dig, acc, cnt = pxb.run(cfg, first, n, want_acceptors=want_acc)
+    eres, edig, eacc, ecnt = oracle_c.run_cpu(cfg, first, n, threads=THREADS, want_acceptors=want_acc)
+    bad = np.nonzero((res != eres).any(axis=1))[0]
+    assert bad.size == 0, "first mismatching instance %d: gpu %s oracle %s" % (
+        first + bad[0], res[bad[0]], eres[bad[0]])
+    assert np.array_equal(dig, edig)
+    if want_acc:
+        assert np.array_equal(acc, eacc)
+    assert cnt == ecnt
+    return res, cnt
+
+
+@pytest.mark.parametrize("c,n", [(1, 8192), (2, 262144), (3, 65536), (4, 8192), (5, 16384)])
+def test_configs_match_oracle(gpu_lib, c, n):
+    _cmp(pxb.CONFIGS[c], 0, n)
+
+
+@pytest.mark.parametrize("path", sorted(p for p in os.listdir(GOLDEN) if p.endswith(".npz")))
+def test_golden_fixtures(gpu_lib, path):
+    z = np.load(os.path.join(GOLDEN, path))
+    c, first, n = (int(x) for x in z["meta"])
+    res, dig, acc, cnt = pxb.run(pxb.CONFIGS[c], first, n, want_acceptors=True)
+    assert np.array_equal(res, z["results"])
+    assert np.array_equal(dig, z["digests"])
+    assert np.array_equal(acc, z["acceptors"])
+    assert cnt["canon_bytes"] == int(z["canon_bytes"][0])
+
+
+@pytest.mark.parametrize("P", [1, 2, 3])
+@pytest.mark.parametrize("N", [2, 3, 4, 5, 6, 7, 8, 9])
+def test_topology_sweep(gpu_lib, P, N):
+    cfg = pxb.Config(seed=0x1234 + 16 * P + N, n_proposers=P, n_acceptors=N, loss_ppm=150000,
+                     delay_max=5, skew_max=2, crash_ppm=150000, crash_len_max=8,
+                     crash_start_max=6, step_cap=200)
+    _cmp(cfg, 1000, 3001)
+
+
+@pytest.mark.parametrize("kw", [
+    dict(loss_ppm=0, delay_max=15),                 # max delay, FIFO max() rule
+    dict(loss_ppm=1000000),                          # everything lost
+    dict(loss_ppm=500000, step_cap=1),               # cap at the first step
+    dict(crash_ppm=1000000, crash_len_max=1, crash_start_max=0),
+    dict(skew_max=4096, step_cap=8192),              # long idle gaps
+    dict(loss_ppm=350000, delay_max=15, step_cap=8192),
+])
+def test_edge_schedules(gpu_lib, kw):
+    base = dict(seed=99, n_proposers=2, n_acceptors=5)
+    base.update(kw)
+    _cmp(pxb.Config(**base), 0, 2000)
+
+
+@pytest.mark.parametrize("n", [1, 7, 63, 64, 65, 1000])
+def test_ragged_batch_sizes(gpu_lib, n):
+    _cmp(pxb.CONFIGS[3], 5, n)
+
+
+def test_instance_ids_cross_32bit(gpu_lib):
+    _cmp(pxb.CONFIGS[3], (1 << 32) - 3000, 6000)
+
+
+def test_empty_batch(gpu_lib):
+    res, dig, acc, cnt = pxb.run(pxb.CONFIGS[2], 0, 0)
+    assert cnt["instances"] == 0
+
+
+def test_shard_invariance(gpu_lib):
+    """Results depend only on (seed, global instance id): sharded runs
+    concatenate to the unsharded run (the multi-GPU contract)."""
+    cfg = pxb.CONFIGS[5]
+    n = 40000
+    full, dfull, _, cfull = pxb.run(cfg, 0, n)
+    parts, cnts = [], []
+    for k in range(4):
+        r, d, _, c = pxb.run(cfg, k * n // 4, n // 4)
+        parts.append((r, d))
+        cnts.append(c)
+    assert np.array_equal(full, np.concatenate([p[0] for p in parts]))
+    assert np.array_equal(dfull, np.concatenate([p[1] for p in parts]))
+    for key in cfull:
+        assert cfull[key] == sum(c[key] for c in cnts)
+
+
+def test_config2_full_size_properties(gpu_lib):
+    """BASELINE config 2 at full size (2^20): every instance decides c1.1 at
+    ticket 1 in one round, 6 steps, no flag; totals = closed forms."""
+    n = pxb.CONFIG_INSTANCES[2]
+    res, dig, _, cnt = pxb.run(pxb.CONFIGS[2], 0, n)
+    assert (res[:, 0] == pxb.command(1, 1)).all() and (res[:, 1] == 1).all()
+    assert (res[:, 2] == 1).all() and (res[:, 3] == (6 << 16)).all()
+    assert (dig == dig[0, 0]).all()
+    assert cnt["decided"] == n and cnt["messages"] == 25 * n
+    assert cnt["canon_bytes"] == pxb.canonical_bytes_nofault(5) * n
+
+
+def test_config3_full_size_sampled(gpu_lib):
+    """BASELINE config 3 at full size (2^24): a random sample of instances
+    checked against the oracle, plus counter consistency."""
+    cfg = pxb.CONFIGS[3]
+    n = pxb.CONFIG_INSTANCES[3]
+    res, dig, _, cnt = pxb.run(cfg, 0, n)
+    assert cnt["instances"] == n and cnt["decided"] + cnt["undecided"] == n
+    flags = res[:, 3] & 0xFF
+    assert cnt["undecided"] == int(((flags & pxb.F_UNDECIDED) != 0).sum())
+    assert cnt["divergence"] == int(((flags & pxb.F_LOG_DIVERGENCE) != 0).sum())
+    assert cnt["rounds"] == int(res[:, 2].astype(np.int64).sum())
+    rng = np.random.default_rng(3)
+    for i in rng.choice(n, 64, replace=False):
+        eres, edig, _, _ = oracle_c.run_cpu(cfg, int(i), 1)
+        assert np.array_equal(res[i], eres[0]) and np.array_equal(dig[i], edig[0])
+
+
+def test_device_entry_accumulates_totals(gpu_lib):
+    import torch
+    cfg = pxb.CONFIGS[3]
+    n = 10000
+    tot = torch.zeros(16, dtype=torch.int64, device="cuda")
+    out = torch.zeros((n, 4), dtype=torch.int32, device="cuda")
+    pxb.run_device(cfg, 0, n, d_results=out, d_totals=tot)
+    pxb.run_device(cfg, n, n, d_totals=tot)
+    torch.cuda.synchronize()
+    _, _, _, c1 = oracle_c.run_cpu(cfg, 0, 2 * n, threads=THREADS)
+    assert pxb.counters_dict(tot.cpu().tolist()) == c1
+    eres, _, _, _ = oracle_c.run_cpu(cfg, 0, n, threads=THREADS)
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), eres)
+
+
+# ---- single-handler hooks: the kernel's device functions vs oracle handlers --
+def test_acceptor_hook_matches_oracle(gpu_lib):
+    rng = np.random.default_rng(1)
+    n = 20000
+    st = np.zeros((n, 4), np.uint32)
+    st[:, 0] = rng.integers(0, 8, n)
+    st[:, 1] = rng.integers(0, 8, n)
+    st[:, 2] = np.where(rng.random(n) < 0.5, 0, (rng.integers(1, 4, n) << 24) | 1)
+    st[:, 3] = rng.integers(0, 5, n) | (np.where(rng.random(n) < 0.1, 1, 0) << 31).astype(np.uint32)
+    msg = np.zeros((n, 4), np.uint32)
+    msg[:, 0] = rng.integers(0, 3, n)
+    msg[:, 1] = rng.integers(0, 9, n)
+    msg[:, 3] = (rng.integers(1, 4, n) << 24) | 1
+    est, erep = oracle_c.acceptor_handle(st, msg)
+    gst = st.copy()
+    grep = pxb.acceptor_handle(gst, msg)
+    assert np.array_equal(gst, est) and np.array_equal(grep, erep)
+
+
+def test_proposer_hook_matches_oracle(gpu_lib):
+    rng = np.random.default_rng(2)
+    n = 20000
+    st = np.zeros((n, 10), np.uint32)
+    st[:, 0] = rng.integers(0, 8, n)                       # ticket
+    st[:, 1] = (rng.integers(1, 4, n) << 24) | 1           # cmd
+    st[:, 2] = rng.integers(0, 5, n)                       # acks
+    st[:, 3] = rng.integers(0, 3, n)                       # state
+    st[:, 4] = rng.integers(0, 8, n)                       # mr_t
+    st[:, 5] = np.where(rng.random(n) < 0.5, 0, (rng.integers(1, 4, n) << 24) | 1)
+    st[:, 6] = st[:, 0]
+    st[:, 7] = (rng.integers(1, 4, n) << 24) | 1
+    st[:, 8] = rng.integers(0, 2, n)
+    st[:, 9] = rng.integers(1, 4, n)
+    msg = np.zeros((n, 4), np.uint32)
+    msg[:, 0] = rng.integers(0, 4, n)                      # 3 = Tick
+    msg[:, 1] = rng.integers(0, 9, n)
+    msg[:, 2] = rng.integers(0, 8, n)
+    msg[:, 3] = np.where(rng.random(n) < 0.4, 0, (rng.integers(1, 4, n) << 24) | 1)
+    for N in (2, 3, 5, 9):
+        est, ebc, enb = oracle_c.proposer_handle(st, N, msg)
+        gst = st.copy()
+        gbc, gnb = pxb.proposer_handle(gst, N, msg)
+        assert np.array_equal(gst, est) and np.array_equal(gbc, ebc) and np.array_equal(gnb, enb)
