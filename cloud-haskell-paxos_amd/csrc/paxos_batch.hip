@@ -337,36 +337,156 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
       const uint64_t anyb = __ballot(cnt_p > 0u);
       if (anyb != 0ull) {
         stepped = stepped || ((anyb & gmask) != 0ull);
-        // Serial fold in canonical order (acceptor aa, then link seq): every
-        // lane of the slot reads the head of lane aa's link (ds_bpermute) and
-        // applies handleServerResponse (Client.hs:125-189); lane aa pops it.
-#pragma unroll 1
-        for (int aa = 0; aa < N; ++aa) {
-          uint32_t ca = (uint32_t)__shfl((int)cnt_p, base + aa);
-          while (__any(ca > 0u)) {
-            const bool take = ca > 0u;
-            const uint32_t mine = L.sq[p][l_head(Sx[p])][lane];
-            const uint32_t w = (uint32_t)__shfl((int)mine, base + aa);
+        const uint64_t multi = __ballot(cnt_p > 1u);
+        const bool slot_serial = (multi & gmask) != 0ull;
+        // ---- fast path: every link a -> p of the slot has <= 1 due response.
+        // The serial fold of Client.hs:125-189 over acceptors 0..N-1 is done in
+        // rounds, one per state-changing event (majority or NACK):
+        // acks = __ballot + popcount, the majority acceptor = the lane whose
+        // prefix popcount hits the quorum, MostRecent (Common.hs:61-65) = a
+        // slot max-reduction of (t_store, -lane) over the counted acks.
+        const bool fast = pact && !slot_serial && ((anyb & gmask) != 0ull);
+        if (__any(fast)) {
+          const bool has = fast && cnt_p == 1u;
+          const uint32_t w = has ? L.sq[p][l_head(Sx[p])][lane] : 0u;
+          const uint32_t kind = w >> 30;
+          const int32_t x = (int32_t)(w & 0x3FFFu);
+          const int32_t y = (int32_t)((w >> 14) & 0x3FFFu);
+          const uint32_t z = (w >> 28) & 3u;
+          const uint64_t lt = (1ull << lane) - 1ull;
+          uint64_t rem = __ballot(has) & gmask;   // slot's unprocessed responses
+          bool go = fast;
+          while (__any(go)) {
+            const uint32_t rs = S[p].rs;
+            const int32_t T = S[p].ticket;
+            const bool mine = go && ((rem >> lane) & 1ull) != 0ull;
+            const bool is_ack = mine && ((rs == ROUND1 && kind == R1OK && x == T) ||
+                                         (rs == ROUND2 && kind == R2S));
+            const bool is_ab = mine && rs != IDLE && kind == HAVE && x >= T;
+            const uint64_t ackm = __ballot(is_ack) & gmask;
+            const uint64_t abm = __ballot(is_ab) & gmask;
+            const uint32_t need = (uint32_t)(N >> 1) + 1u - S[p].acks;
+            const bool is_maj = is_ack && (uint32_t)__popcll(ackm & lt) + 1u == need;
+            const uint64_t majm = __ballot(is_maj) & gmask;
+            const int e_ab = abm ? __builtin_ctzll(abm) : 64;
+            const int e_mj = majm ? __builtin_ctzll(majm) : 64;
+            const int e = min(e_ab, e_mj);
+            const uint64_t below_e = (e >= 64) ? ~0ull : ((1ull << e) - 1ull);
+            const uint64_t counted = (ackm & below_e) | ((e_mj < e_ab) ? (1ull << e_mj) : 0ull);
+            // MostRecent over the counted Round1OKs that carry a proposal
+            const bool elig = rs == ROUND1 && ((counted >> lane) & 1ull) != 0ull && z != 0u;
+            const uint64_t zb = __ballot(elig) & gmask;
+            uint32_t key = elig ? (((uint32_t)y << 5) | (31u - (uint32_t)a)) : 0u;
+            if (__any(__popcll(zb) > 1)) {
+#pragma unroll
+              for (int off = 1; off < N; off <<= 1) {
+                const uint32_t o = (uint32_t)__shfl((int)key, lane + off);
+                if (a + off < N) key = max(key, o);
+              }
+            }
+            const int src = zb ? ((__popcll(zb) > 1) ? base : __builtin_ctzll(zb)) : lane;
+            key = (uint32_t)__shfl((int)key, src);
+            const int wl = base + 31 - (int)(key & 31u);
+            const uint32_t bz = (uint32_t)__shfl((int)z, zb ? wl : lane);
+            const uint32_t u = (uint32_t)__shfl(x, e_ab < 64 ? e_ab : lane);
             Req o0{NONE, 0, 0}, o1{NONE, 0, 0};
             uint32_t no = 0;
-            if (take) {
-              const uint32_t kind = w >> 30;
-              no = proposer_step(S[p], (uint32_t)N, kind, (int32_t)(w & 0x3FFFu),
-                                 (int32_t)((w >> 14) & 0x3FFFu), (w >> 28) & 3u, o0, o1);
-              if (a == aa) {
-                canon_acc += 2u * (16u >> kind);
-                link_pop(Sx[p]);
+            if (go) {
+              PropState& Sp = S[p];
+              int32_t mt = Sp.mr_t;
+              uint32_t mv = Sp.mr_v;
+              if (zb != 0ull && (mv == 0u || (int32_t)(key >> 5) > mt)) {
+                mt = (int32_t)(key >> 5);
+                mv = bz;
               }
-              ca--;
+              Sp.acks += (uint32_t)__popcll(counted);
+              if (e >= 64) {                       // no event: only acks
+                if (rs == ROUND1) {
+                  Sp.mr_t = mt;
+                  Sp.mr_v = mv;
+                }
+                go = false;
+              } else if (e_mj < e_ab) {            // majority reached at lane e
+                if (rs == ROUND1) {                // Client.hs:157-170
+                  Sp.r2_t = T;
+                  Sp.r2_v = (mv == 0u) ? Sp.cmd : mv;
+                  Sp.pending = (mv != 0u);
+                  Sp.acks = 0;
+                  Sp.rs = ROUND2;
+                  Sp.mr_t = 0;
+                  Sp.mr_v = 0;
+                  o0 = Req{PROPOSE, T, Sp.r2_v};
+                  no = 1;
+                } else {                           // Client.hs:177-189
+                  o0 = Req{EXECUTE, T, 0};
+                  if (Sp.pending) {
+                    Sp.ticket = T + 1;
+                    Sp.acks = 0;
+                    Sp.rs = ROUND1;
+                    Sp.mr_t = 0;
+                    Sp.mr_v = 0;
+                    o1 = Req{ASK, T + 1, 0};
+                    no = 2;
+                  } else {
+                    Sp.cmd = 0;
+                    Sp.acks = 0;
+                    Sp.rs = IDLE;
+                    no = 1;
+                  }
+                }
+              } else {                             // HaveTicket u >= ticket, Client.hs:130-140
+                Sp.ticket = (int32_t)u + 1;
+                Sp.acks = 0;
+                Sp.rs = ROUND1;
+                Sp.mr_t = 0;
+                Sp.mr_v = 0;
+                o0 = Req{ASK, (int32_t)u + 1, 0};
+                no = 1;
+              }
+              if (e < 64) {
+                rem &= ~(below_e | (1ull << e));
+                if (rem == 0ull) go = false;
+              }
             }
 #pragma unroll 1
             for (uint32_t k = 0; k < 2u; ++k) {
-              const bool has = no > k;
-              if (__any(has)) {
-                const uint32_t kk = k ? o1.kind : o0.kind;
-                const int32_t kx = k ? o1.x : o0.x;
-                const uint32_t kz = k ? o1.z : o0.z;
-                send_req(pc, has, kk, kx, kz);
+              const bool hs = no > k;
+              if (__any(hs)) send_req(pc, hs, k ? o1.kind : o0.kind, k ? o1.x : o0.x, k ? o1.z : o0.z);
+            }
+          }
+          if (has) {
+            canon_acc += 2u * (16u >> kind);
+            link_pop(Sx[p]);
+          }
+        }
+        // ---- general path (a link holds >= 2 due responses): serial fold in
+        // canonical order; every lane of the slot reads the head of lane aa's
+        // link (ds_bpermute) and applies handleServerResponse; lane aa pops it.
+        const uint32_t cnt_s = slot_serial ? cnt_p : 0u;
+        if (__any(cnt_s > 0u)) {
+#pragma unroll 1
+          for (int aa = 0; aa < N; ++aa) {
+            uint32_t ca = (uint32_t)__shfl((int)cnt_s, base + aa);
+            while (__any(ca > 0u)) {
+              const bool take = ca > 0u;
+              const uint32_t mine = L.sq[p][l_head(Sx[p])][lane];
+              const uint32_t w = (uint32_t)__shfl((int)mine, base + aa);
+              Req o0{NONE, 0, 0}, o1{NONE, 0, 0};
+              uint32_t no = 0;
+              if (take) {
+                const uint32_t kind = w >> 30;
+                no = proposer_step(S[p], (uint32_t)N, kind, (int32_t)(w & 0x3FFFu),
+                                   (int32_t)((w >> 14) & 0x3FFFu), (w >> 28) & 3u, o0, o1);
+                if (a == aa) {
+                  canon_acc += 2u * (16u >> kind);
+                  link_pop(Sx[p]);
+                }
+                ca--;
+              }
+#pragma unroll 1
+              for (uint32_t k = 0; k < 2u; ++k) {
+                const bool hs = no > k;
+                if (__any(hs)) send_req(pc, hs, k ? o1.kind : o0.kind, k ? o1.x : o0.x, k ? o1.z : o0.z);
               }
             }
           }
@@ -381,14 +501,14 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
 #pragma unroll
     for (int p = 0; p < PM; ++p) busy = busy || ((R[p].hl | Sx[p].hl) & 0x78u) != 0u;
     const uint64_t busyb = __ballot(active && busy);
-    const uint64_t pan = __ballot((lflags & PXB_F_PANIC) != 0u);
-    const uint64_t dvg = __ballot((lflags & PXB_F_LOG_DIVERGENCE) != 0u);
-    const uint64_t qov = __ballot((lflags & PXB_F_QUEUE_OVERFLOW) != 0u);
-    const uint64_t trc = __ballot((lflags & PXB_F_LOG_TRUNC) != 0u);
-    if (active) {
-      const bool quiet = ((busyb & gmask) == 0ull) && s >= last_tick;
-      const bool cap = !quiet && (s + 1 >= (int32_t)kp.step_cap);
-      s++;
+    const bool quiet = active && ((busyb & gmask) == 0ull) && s >= last_tick;
+    const bool cap = active && !quiet && (s + 1 >= (int32_t)kp.step_cap);
+    if (active) s++;
+    if (__any(quiet || cap)) {
+      const uint64_t pan = __ballot((lflags & PXB_F_PANIC) != 0u);
+      const uint64_t dvg = __ballot((lflags & PXB_F_LOG_DIVERGENCE) != 0u);
+      const uint64_t qov = __ballot((lflags & PXB_F_QUEUE_OVERFLOW) != 0u);
+      const uint64_t trc = __ballot((lflags & PXB_F_LOG_TRUNC) != 0u);
       if (quiet || cap) {
         uint32_t f = tflags;
         if (pan & gmask) f |= PXB_F_PANIC;
