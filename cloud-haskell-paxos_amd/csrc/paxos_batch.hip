@@ -65,6 +65,7 @@ struct KParams {
   uint32_t* dig;
   pxb_acceptor_rec* acc;
   unsigned long long* totals;
+  unsigned long long* dbg;        // diagnostic builds only (PXB_STAMPS)
 };
 
 __host__ __device__ inline uint64_t prob_threshold(uint32_t ppm) {
@@ -79,6 +80,27 @@ __device__ __forceinline__ void static_for(F&& f) {
     static_for<I + 1, E>(f);
   }
 }
+
+// ---- diagnostic section stamps (separate build: -DPXB_STAMPS; never timed) --
+#ifdef PXB_STAMPS
+#define STAMP_DECL uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; uint64_t st_prev = __builtin_amdgcn_s_memtime();
+#define STAMP(i)                                                  \
+  do {                                                            \
+    __builtin_amdgcn_sched_barrier(0);                            \
+    const uint64_t st_now = __builtin_amdgcn_s_memtime();         \
+    __builtin_amdgcn_sched_barrier(0);                            \
+    st_acc[i] += st_now - st_prev;                                \
+    st_prev = st_now;                                             \
+  } while (0)
+#define STAMP_FLUSH(ptr)                                          \
+  if (lane == 0 && (ptr)) {                                       \
+    for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&(ptr)[i_], (unsigned long long)st_acc[i_]); \
+  }
+#else
+#define STAMP_DECL
+#define STAMP(i) do {} while (0)
+#define STAMP_FLUSH(ptr)
+#endif
 
 // ---- one directed link = LDS ring (payload) + 3 registers ------------------
 // Tickets never exceed step_cap (<= 8192 < 2^14: a proposer's ticket grows by
@@ -110,8 +132,8 @@ struct Lds {
   static constexpr int G = 64 / N;
   uint32_t rq[PM][QD][64];       // links p -> a   (lane-interleaved: conflict-free)
   uint32_t sq[PM][QD][64];       // links a -> p
-  uint32_t clog[G][LT];          // per-slot canonical log (divergence check)
-  uint32_t cnt[PXB_NCOUNTERS];
+  uint32_t clog[G][LT + 1];      // per-slot canonical log (+1 pad: rows on distinct banks);
+                                 // entries are (epoch << 2 | command), epoch = instance tag
 };
 
 // occupancy target (waves per SIMD) by proposer count: bounds the VGPR budget
@@ -134,12 +156,13 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
   const uint64_t gmask = used ? ((((1ull << N) - 1ull)) << base) : 0ull;
   const uint64_t below = (1ull << base) - 1ull;      // base <= 63
   uint32_t* clog = &L.clog[used ? g : 0][0];
-  if (lane < PXB_NCOUNTERS) L.cnt[lane] = 0;
+  for (int k = lane; k < G * (LT + 1); k += 64) (&L.clog[0][0])[k] = 0u;   // epoch 0 = empty
 
   const uint64_t wave = (uint64_t)blockIdx.x * WPB + wib;
   const uint64_t nwaves = (uint64_t)gridDim.x * WPB;
   const uint64_t n = kp.n_instances;
   uint64_t next = n * wave / nwaves;
+  const uint64_t first_idx = next;
   const uint64_t end = n * (wave + 1) / nwaves;
   const uint32_t k0 = kp.k0, k1 = kp.k1;
 
@@ -166,6 +189,11 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
   bool decided = false;
   uint32_t msgs_acc = 0;                  // lane totals across instances
   uint64_t canon_acc = 0;
+  uint32_t rounds_acc = 0, steps_acc = 0; // slot leaders
+  uint32_t wc[PXB_NCOUNTERS];             // wave-uniform counts (ballot + popcount)
+#pragma unroll
+  for (int i = 0; i < PXB_NCOUNTERS; ++i) wc[i] = 0;
+  uint32_t tag = 0;                       // canonical-log epoch of the slot's instance
 #pragma unroll
   for (int p = 0; p < PM; ++p) {
     skew[p] = 0;
@@ -186,17 +214,14 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
       ok = (uint64_t)w.x >= loss_thr;
       d = 1 + (int32_t)mulhi_n(w.y, delay_max);
     }
-    if (ok) {
-      const uint32_t len = l_len(Lk);
-      if (len >= (uint32_t)QD) {
-        lflags |= PXB_F_QUEUE_OVERFLOW;
-      } else {
-        const int32_t due = max(s + d, l_last(Lk));
-        ring[((l_head(Lk) + len) & 7u) * 64u + (uint32_t)lane] = word;
-        Lk.dn |= ((uint32_t)due & 15u) << (4u * len);
-        Lk.hl = (Lk.hl & 7u) | ((len + 1u) << 3) | ((uint32_t)due << 8);
-      }
-    }
+    const uint32_t len = l_len(Lk);
+    const bool full = len >= (uint32_t)QD;
+    const bool push = ok && !full;
+    lflags |= (ok && full) ? (uint32_t)PXB_F_QUEUE_OVERFLOW : 0u;
+    const int32_t due = max(s + d, l_last(Lk));
+    if (push) ring[((l_head(Lk) + len) & 7u) * 64u + (uint32_t)lane] = word;
+    Lk.dn = push ? (Lk.dn | (((uint32_t)due & 15u) << (4u * len))) : Lk.dn;
+    Lk.hl = push ? ((Lk.hl & 7u) | ((len + 1u) << 3) | ((uint32_t)due << 8)) : Lk.hl;
   };
   auto link_pop = [&](Link& Lk) {
     Lk.dn >>= 4;
@@ -216,6 +241,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
               ((uint32_t)x & 0x3FFFu) | (z << 14) | (kind << 16));
   };
 
+  STAMP_DECL
   for (;;) {
     // ---------------- refill free slots from this wave's range -------------
     const uint64_t freeb = __ballot(used && !active && a == 0);
@@ -268,12 +294,13 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
         dtick = 0;
         decided = false;
         s = 0;
-        for (int k = a; k < LT; k += N) clog[k] = 0u;
+        tag = (uint32_t)(cand - first_idx) + 1u;
         active = true;
       }
       next = min(next + (uint64_t)__popcll(freeb), end);
     }
     if (!__any(active)) break;
+    STAMP(0);
 
     const uint32_t s4 = (uint32_t)s & 15u;
     // ---------------- acceptor phase: (proposer index, link seq) order -------
@@ -302,8 +329,11 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
               if (ev != 0u) {
                 digest = fnv_u32(digest, (ev << 24) | 1u);
                 if (log_len < (uint32_t)LT) {
-                  const uint32_t old = atomicCAS(&clog[log_len], 0u, ev);
-                  if (old != 0u && old != ev) lflags |= PXB_F_LOG_DIVERGENCE;
+                  // two acceptors of this instance executed different commands at
+                  // the same position iff the max already holds this epoch with
+                  // another command (order-independent, SEMANTICS §7)
+                  const uint32_t old = atomicMax(&clog[log_len], (tag << 2) | ev);
+                  if ((old >> 2) == tag && (old & 3u) != ev) lflags |= PXB_F_LOG_DIVERGENCE;
                 } else {
                   lflags |= PXB_F_LOG_TRUNC;
                 }
@@ -318,6 +348,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
       });
     }
 
+    STAMP(1);
     // ---------------- proposer phase: Tick, then (acceptor, link seq) order --
     static_for<0, PM>([&](auto pc) {
       constexpr int p = decltype(pc)::value;
@@ -346,6 +377,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
         // prefix popcount hits the quorum, MostRecent (Common.hs:61-65) = a
         // slot max-reduction of (t_store, -lane) over the counted acks.
         const bool fast = pact && !slot_serial && ((anyb & gmask) != 0ull);
+        STAMP(2);
         if (__any(fast)) {
           const bool has = fast && cnt_p == 1u;
           const uint32_t w = has ? L.sq[p][l_head(Sx[p])][lane] : 0u;
@@ -377,18 +409,22 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
             const bool elig = rs == ROUND1 && ((counted >> lane) & 1ull) != 0ull && z != 0u;
             const uint64_t zb = __ballot(elig) & gmask;
             uint32_t key = elig ? (((uint32_t)y << 5) | (31u - (uint32_t)a)) : 0u;
-            if (__any(__popcll(zb) > 1)) {
+            uint32_t bz = 0;
+            if (__any(zb != 0ull)) {            // some slot saw a stored proposal
+              if (__any(__popcll(zb) > 1)) {
 #pragma unroll
-              for (int off = 1; off < N; off <<= 1) {
-                const uint32_t o = (uint32_t)__shfl((int)key, lane + off);
-                if (a + off < N) key = max(key, o);
+                for (int off = 1; off < N; off <<= 1) {
+                  const uint32_t o = (uint32_t)__shfl((int)key, lane + off);
+                  if (a + off < N) key = max(key, o);
+                }
               }
+              const int src = zb ? ((__popcll(zb) > 1) ? base : __builtin_ctzll(zb)) : lane;
+              key = (uint32_t)__shfl((int)key, src);
+              const int wl = base + 31 - (int)(key & 31u);
+              bz = (uint32_t)__shfl((int)z, zb ? wl : lane);
             }
-            const int src = zb ? ((__popcll(zb) > 1) ? base : __builtin_ctzll(zb)) : lane;
-            key = (uint32_t)__shfl((int)key, src);
-            const int wl = base + 31 - (int)(key & 31u);
-            const uint32_t bz = (uint32_t)__shfl((int)z, zb ? wl : lane);
-            const uint32_t u = (uint32_t)__shfl(x, e_ab < 64 ? e_ab : lane);
+            uint32_t u = 0;
+            if (__any(abm != 0ull)) u = (uint32_t)__shfl(x, e_ab < 64 ? e_ab : lane);
             Req o0{NONE, 0, 0}, o1{NONE, 0, 0};
             uint32_t no = 0;
             if (go) {
@@ -462,6 +498,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
         // ---- general path (a link holds >= 2 due responses): serial fold in
         // canonical order; every lane of the slot reads the head of lane aa's
         // link (ds_bpermute) and applies handleServerResponse; lane aa pops it.
+        STAMP(3);
         const uint32_t cnt_s = slot_serial ? cnt_p : 0u;
         if (__any(cnt_s > 0u)) {
 #pragma unroll 1
@@ -496,6 +533,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
       if (pact && S[p].ticket >= PXB_TICKET_LIMIT) tflags |= PXB_F_TICKET_OVERFLOW;
     });
 
+    STAMP(4);
     // ---------------- end of step: quiescence / step cap ---------------------
     bool busy = false;
 #pragma unroll
@@ -504,50 +542,48 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
     const bool quiet = active && ((busyb & gmask) == 0ull) && s >= last_tick;
     const bool cap = active && !quiet && (s + 1 >= (int32_t)kp.step_cap);
     if (active) s++;
-    if (__any(quiet || cap)) {
+    const bool done = quiet || cap;
+    if (__any(done)) {
       const uint64_t pan = __ballot((lflags & PXB_F_PANIC) != 0u);
       const uint64_t dvg = __ballot((lflags & PXB_F_LOG_DIVERGENCE) != 0u);
       const uint64_t qov = __ballot((lflags & PXB_F_QUEUE_OVERFLOW) != 0u);
       const uint64_t trc = __ballot((lflags & PXB_F_LOG_TRUNC) != 0u);
-      if (quiet || cap) {
-        uint32_t f = tflags;
-        if (pan & gmask) f |= PXB_F_PANIC;
-        if (dvg & gmask) f |= PXB_F_LOG_DIVERGENCE;
-        if (qov & gmask) f |= PXB_F_QUEUE_OVERFLOW;
-        if (trc & gmask) f |= PXB_F_LOG_TRUNC;
-        if (cap) f |= PXB_F_STEP_CAP;
-        if (!decided) f |= PXB_F_UNDECIDED;
-        if (!cap) {
+      uint32_t f = tflags;
+      f |= (pan & gmask) ? (uint32_t)PXB_F_PANIC : 0u;
+      f |= (dvg & gmask) ? (uint32_t)PXB_F_LOG_DIVERGENCE : 0u;
+      f |= (qov & gmask) ? (uint32_t)PXB_F_QUEUE_OVERFLOW : 0u;
+      f |= (trc & gmask) ? (uint32_t)PXB_F_LOG_TRUNC : 0u;
+      f |= cap ? (uint32_t)PXB_F_STEP_CAP : 0u;
+      f |= decided ? 0u : (uint32_t)PXB_F_UNDECIDED;
 #pragma unroll
-          for (int p = 0; p < PM; ++p)
-            if ((uint32_t)p < P && S[p].rs != IDLE) f |= PXB_F_STUCK;
-        }
+      for (int p = 0; p < PM; ++p)
+        f |= (!cap && (uint32_t)p < P && S[p].rs != IDLE) ? (uint32_t)PXB_F_STUCK : 0u;
+      const bool lead = done && a == 0;
+      // run totals: one ballot + popcount per counter over the finishing slots
+      wc[PXB_C_INSTANCES] += (uint32_t)__popcll(__ballot(lead));
+      wc[PXB_C_UNDECIDED] += (uint32_t)__popcll(__ballot(lead && (f & PXB_F_UNDECIDED)));
+      if (__any(lead && (f & ~(uint32_t)PXB_F_UNDECIDED) != 0u)) {
+        wc[PXB_C_STUCK] += (uint32_t)__popcll(__ballot(lead && (f & PXB_F_STUCK)));
+        wc[PXB_C_PANIC] += (uint32_t)__popcll(__ballot(lead && (f & PXB_F_PANIC)));
+        wc[PXB_C_DIVERGENCE] += (uint32_t)__popcll(__ballot(lead && (f & PXB_F_LOG_DIVERGENCE)));
+        wc[PXB_C_STEP_CAP] += (uint32_t)__popcll(__ballot(lead && (f & PXB_F_STEP_CAP)));
+        wc[PXB_C_QUEUE_OVERFLOW] += (uint32_t)__popcll(__ballot(lead && (f & PXB_F_QUEUE_OVERFLOW)));
+        wc[PXB_C_TICKET_OVERFLOW] += (uint32_t)__popcll(__ballot(lead && (f & PXB_F_TICKET_OVERFLOW)));
+        wc[PXB_C_LOG_TRUNC] += (uint32_t)__popcll(__ballot(lead && (f & PXB_F_LOG_TRUNC)));
+      }
+      if (done) {
         const uint32_t steps = (uint32_t)s;
-        if (a == 0) {
-          if (kp.out) {
-            uint4 r;
-            r.x = decided ? ((dval << 24) | 1u) : 0u;
-            r.y = decided ? (uint32_t)dtick : 0u;
-            r.z = rounds;
-            r.w = (f & 0xFFu) | (min(steps, 0xFFFFu) << 16);
-            *reinterpret_cast<uint4*>(kp.out + idx) = r;
-          }
-          uint32_t* cnt = L.cnt;
-          atomicAdd(&cnt[PXB_C_DECIDED], decided ? 1u : 0u);
-          atomicAdd(&cnt[PXB_C_UNDECIDED], decided ? 0u : 1u);
-          if (f & PXB_F_STUCK) atomicAdd(&cnt[PXB_C_STUCK], 1u);
-          if (f & PXB_F_PANIC) atomicAdd(&cnt[PXB_C_PANIC], 1u);
-          if (f & PXB_F_LOG_DIVERGENCE) atomicAdd(&cnt[PXB_C_DIVERGENCE], 1u);
-          if (f & PXB_F_STEP_CAP) atomicAdd(&cnt[PXB_C_STEP_CAP], 1u);
-          if (f & PXB_F_QUEUE_OVERFLOW) atomicAdd(&cnt[PXB_C_QUEUE_OVERFLOW], 1u);
-          if (f & PXB_F_TICKET_OVERFLOW) atomicAdd(&cnt[PXB_C_TICKET_OVERFLOW], 1u);
-          if (f & PXB_F_LOG_TRUNC) atomicAdd(&cnt[PXB_C_LOG_TRUNC], 1u);
-          atomicAdd(&cnt[PXB_C_ROUNDS], rounds);
-          atomicAdd(&cnt[PXB_C_STEPS], steps);
-          atomicAdd(&cnt[PXB_C_INSTANCES], 1u);
-          canon_acc += 16u;
+        rounds_acc += lead ? rounds : 0u;
+        steps_acc += lead ? steps : 0u;
+        canon_acc += lead ? 20u : 4u;                 // result record + this digest
+        if (lead && kp.out) {
+          uint4 r;
+          r.x = decided ? ((dval << 24) | 1u) : 0u;
+          r.y = decided ? (uint32_t)dtick : 0u;
+          r.z = rounds;
+          r.w = (f & 0xFFu) | (min(steps, 0xFFFFu) << 16);
+          *reinterpret_cast<uint4*>(kp.out + idx) = r;
         }
-        canon_acc += 4u;
         if (kp.dig) kp.dig[idx * N + a] = fnv_u32(digest, log_len);
         if (kp.acc) {
           uint4 r;
@@ -560,25 +596,33 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
         active = false;
       }
     }
+    STAMP(5);
   }
 
+  STAMP(6);
+  STAMP_FLUSH(kp.dbg);
   // ---------------- flush wave totals -----------------------------------------
-  uint32_t m = msgs_acc;
+  uint32_t m = msgs_acc, ra = rounds_acc, sa = steps_acc;
   uint64_t c64 = canon_acc;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     m += (uint32_t)__shfl_xor((int)m, off);
+    ra += (uint32_t)__shfl_xor((int)ra, off);
+    sa += (uint32_t)__shfl_xor((int)sa, off);
     const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)c64, off);
     const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(c64 >> 32), off);
     c64 += ((uint64_t)hi << 32) | lo;
   }
+  wc[PXB_C_DECIDED] = wc[PXB_C_INSTANCES] - wc[PXB_C_UNDECIDED];
   if (lane == 0) {
-    atomicAdd(&kp.totals[PXB_C_MESSAGES], (unsigned long long)m);
-    atomicAdd(&kp.totals[PXB_C_CANON_BYTES], (unsigned long long)c64);
-  }
-  if (lane < PXB_NCOUNTERS && lane != PXB_C_MESSAGES && lane != PXB_C_CANON_BYTES) {
-    const uint32_t v = L.cnt[lane];
-    if (v) atomicAdd(&kp.totals[lane], (unsigned long long)v);
+    unsigned long long* T = kp.totals;
+    atomicAdd(&T[PXB_C_MESSAGES], (unsigned long long)m);
+    atomicAdd(&T[PXB_C_CANON_BYTES], (unsigned long long)c64);
+    atomicAdd(&T[PXB_C_ROUNDS], (unsigned long long)ra);
+    atomicAdd(&T[PXB_C_STEPS], (unsigned long long)sa);
+#pragma unroll
+    for (int i = 0; i < PXB_NCOUNTERS; ++i)
+      if (wc[i] != 0u) atomicAdd(&T[i], (unsigned long long)wc[i]);
   }
 }
 
@@ -650,6 +694,9 @@ static kernel_fn pick(uint32_t pm, uint32_t n) {
 }
 
 static thread_local int g_last_hip = 0;
+#ifdef PXB_STAMPS
+static unsigned long long* g_dbg = nullptr;
+#endif
 static std::mutex g_mu;
 static int g_occ[4][10][64];            // [pm][n][device] blocks per CU (0 = unknown)
 static int g_cus[64];
@@ -684,6 +731,17 @@ using namespace pxb;
 extern "C" {
 
 int pxb_abi_version(void) { return PXB_ABI_VERSION; }
+
+#ifdef PXB_STAMPS
+// diagnostic build only: cycles per kernel section summed over waves (and reset)
+int pxb_debug_stamps(unsigned long long* out8) {
+  if (!g_dbg) return PXB_E_INVAL;
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(out8, g_dbg, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemset(g_dbg, 0, 8 * sizeof(unsigned long long)));
+  return PXB_OK;
+}
+#endif
 int pxb_last_hip_error(void) { return g_last_hip; }
 
 const char* pxb_strerror(int code) {
@@ -749,6 +807,17 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
   kp.dig = d_log_digest;
   kp.acc = d_acc;
   kp.totals = reinterpret_cast<unsigned long long*>(d_totals);
+#ifdef PXB_STAMPS
+  {
+    static unsigned long long* dbg = nullptr;
+    if (!dbg) {
+      HIPCHK(hipMalloc(&dbg, 8 * sizeof(unsigned long long)));
+      HIPCHK(hipMemset(dbg, 0, 8 * sizeof(unsigned long long)));
+    }
+    kp.dbg = dbg;
+    g_dbg = dbg;
+  }
+#endif
   const uint64_t G = 64 / cfg->n_acceptors;
   const uint64_t waves_needed = (cfg->n_instances + G - 1) / G;
   const uint64_t blocks_needed = (waves_needed + WPB - 1) / WPB;

@@ -60,43 +60,29 @@ struct AccState {
 };
 
 // Returns the reply tag (or NONE).  exec_val != 0 when `executed <>= [c]` ran.
+// Written as selects (no branches): every lane of a wave may hold a different
+// request kind, and a branchy body costs exec-mask juggling on all of them.
 __device__ __forceinline__ uint32_t acceptor_step(AccState& A, uint32_t kind, int32_t x, uint32_t z,
                                                   int32_t& rx, int32_t& ry, uint32_t& rz,
                                                   uint32_t& exec_val) {
-  exec_val = 0;
-  rx = 0;
-  ry = 0;
-  rz = 0;
-  if (kind == ASK) {                       // Server.hs:54
-    if (A.t_max >= x) {                    // :56  (>=)
-      rx = A.t_max;                        // :58  HaveTicket newestTicket
-      return HAVE;
-    }
-    A.t_max = x;                           // :60
-    rx = x;                                // :61-62 Round1OK reqTicket mP
-    ry = A.t_store;
-    rz = A.val;
-    return R1OK;
-  }
-  if (kind == PROPOSE) {                   // :64
-    if (x == A.t_max) {                    // :66  equality, not >=
-      A.t_store = x;                       // :68
-      A.val = z;
-      return R2S;                          // :69
-    }
-    rx = A.t_max;                          // :71
-    return HAVE;
-  }
-  if (A.t_max == x) {                      // Execute, :73-75
-    if (A.val == 0) {                      // :76 `Just (_, c) <- use proposal` fails
-      A.dead = true;
-      return NONE;
-    }
-    exec_val = A.val;                      // :78  executed <>= [c]
-    A.t_store = 0;                         // :77  proposal .= Nothing
-    A.val = 0;
-  }
-  return NONE;
+  const bool is_ask = kind == ASK;                       // Server.hs:54
+  const bool is_prop = kind == PROPOSE;                  // Server.hs:64
+  const bool is_exec = kind == EXECUTE;                  // Server.hs:73
+  const bool grant = is_ask && !(A.t_max >= x);          // :56  T_max >= t -> HaveTicket
+  const bool accept = is_prop && (x == A.t_max);         // :66  equality, not >=
+  const bool hit = is_exec && (A.t_max == x);            // :75
+  const bool panic = hit && A.val == 0u;                 // :76 `Just (_, c) <-` fails (Q6)
+  const bool run = hit && A.val != 0u;                   // :77-78
+  const uint32_t rk = grant ? R1OK : accept ? R2S : (is_exec ? NONE : HAVE);
+  rx = grant ? x : (accept ? 0 : A.t_max);               // :58/:71 HaveTicket T_max; :62 Round1OK t
+  ry = grant ? A.t_store : 0;                            // :61-62 Round1OK t prop
+  rz = grant ? A.val : 0u;
+  exec_val = run ? A.val : 0u;                           // :78 executed <>= [c]
+  A.t_max = grant ? x : A.t_max;                         // :60
+  A.t_store = accept ? x : (run ? 0 : A.t_store);        // :68 / :77
+  A.val = accept ? z : (run ? 0u : A.val);
+  A.dead = A.dead || panic;
+  return rk;
 }
 
 // ---- proposer: ClientState (Client.hs:58-67) -------------------------------

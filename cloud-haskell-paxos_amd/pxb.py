@@ -20,7 +20,7 @@ from dataclasses import dataclass
 from typing import Optional
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "csrc", "libpaxos_batch.so")
+LIB_PATH = os.environ.get("PXB_LIB") or os.path.join(_HERE, "csrc", "libpaxos_batch.so")
 
 # ---- constants (include/paxos_batch.h) ------------------------------------
 PXB_OK, PXB_E_INVAL, PXB_E_HIP, PXB_E_OOM, PXB_E_NODEV, PXB_E_RCCL = 0, -1, -2, -3, -4, -5
