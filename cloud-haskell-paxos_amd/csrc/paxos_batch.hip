@@ -6,29 +6,35 @@
 //
 //   * lane = (instance slot g, acceptor a): G = 64 / N instance slots per wave,
 //     lanes g*N .. g*N+N-1 hold the N acceptors of one instance (SoA in VGPRs).
+//     The kernel is VALU-issue bound (throughput saturates at 2-3 waves per
+//     SIMD), so state stays unpacked and every hot-path instruction counts.
 //   * each acceptor lane owns its directed links: the request queue from every
 //     proposer p (p -> a) and the response queue to every proposer (a -> p),
-//     PXB_QUEUE_DEPTH deep, as register shift-queues with 4-bit due stamps.
+//     PXB_QUEUE_DEPTH deep, as lane-interleaved LDS rings (bank-conflict free)
+//     with the due steps nibble-packed in one register per link.
 //   * the P proposers of an instance are replicated in all N lanes of its
-//     slot; each response is broadcast to the slot with ds_bpermute and folded
-//     by every lane in canonical (acceptor, link seq) order, so all lanes keep
-//     the same proposer state and each lane enqueues its own copy of a
-//     broadcast on its own link (Philox loss/delay per link, in parallel).
+//     slot.  Responses are folded in canonical (acceptor, link seq) order:
+//     quorum counting with __ballot + popcount, the majority acceptor from a
+//     prefix popcount, MostRecent (Common.hs:61-65) from a slot max-reduction;
+//     a serial ds_bpermute fold handles the rare slot with 2+ due responses on
+//     one link.  Each lane enqueues its own copy of a broadcast on its own
+//     link (Philox loss/delay per link, in parallel).
 //   * waves are persistent: when a slot's instance quiesces (or hits
-//     step_cap) the slot writes its outputs and refills from the wave's
-//     contiguous instance range, so divergent instance lengths do not idle
-//     lanes.
-//   * divergence of acceptor logs is detected with LDS compare-and-swap on a
-//     per-slot canonical log (PXB_LOG_TRACK positions).
+//     step_cap) the slot writes its 16-B result + 4-B/acceptor digests and
+//     refills from the wave's contiguous instance range.
+//   * run totals are reduced from the result records by a second kernel, so
+//     the hot loop carries no counter state.
 //
 // Semantics: docs/SEMANTICS.md; checked bit-exact against oracle/.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <type_traits>
 #include <mutex>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
+#include <type_traits>
 
 #include "../../include/paxos_batch.h"
 #include "paxos_device.h"
@@ -38,8 +44,9 @@ namespace pxb {
 constexpr int QD = PXB_QUEUE_DEPTH;   // 8: ring slots per directed link
 constexpr int LT = PXB_LOG_TRACK;
 static_assert(QD == 8, "due-nibble word and ring masks assume 8 slots");
+static_assert(PXB_MAX_STEP_CAP <= 8192, "14-bit packed tickets / steps");
 #ifndef PXB_WPB
-#define PXB_WPB 2
+#define PXB_WPB 1
 #endif
 constexpr int WPB = PXB_WPB;          // waves per block (LDS is carved per wave)
 constexpr int BLOCK = 64 * WPB;
@@ -53,19 +60,25 @@ constexpr int BLOCK = 64 * WPB;
 #define PXB_OCC_P3 2
 #endif
 
+// kp.cfg bit layout
+constexpr uint32_t CFG_RANDOMIZE = 1u << 0;
+constexpr uint32_t CFG_LOSSY = 1u << 1;     // loss threshold > 0
+constexpr uint32_t CFG_CRASHY = 1u << 2;    // crash threshold > 0
+
 struct KParams {
   uint64_t first_instance;
-  uint64_t n_instances;
-  uint64_t loss_thr;                  // precomputed (non-randomized)
-  uint64_t crash_thr;
-  uint32_t k0, k1;
-  uint32_t n_prop, loss_ppm, delay_max, crash_ppm, crash_len_max, crash_start_max;
-  uint32_t skew_max, step_cap, randomize;
-  pxb_result* out;
+  uint32_t n_instances;               // this launch (host chunks larger batches)
+  uint32_t k0, k1;                    // Philox key = seed
+  uint32_t cfg;                       // CFG_*
+  uint32_t n_prop, delay_max;
+  uint32_t loss_m1, crash_m1;         // thr-1 (valid when LOSSY / CRASHY)
+  uint32_t loss_ppm, crash_ppm;       // maxima for RANDOMIZE
+  uint32_t crash_len_max, crash_start_max, skew_max, step_cap;
+  uint4* out;                         // pxb_result records (never null)
   uint32_t* dig;
-  pxb_acceptor_rec* acc;
+  uint4* acc;
   unsigned long long* totals;
-  unsigned long long* dbg;        // diagnostic builds only (PXB_STAMPS)
+  unsigned long long* dbg;            // diagnostic builds only (PXB_STAMPS)
 };
 
 __host__ __device__ inline uint64_t prob_threshold(uint32_t ppm) {
@@ -103,10 +116,7 @@ __device__ __forceinline__ void static_for(F&& f) {
 #endif
 
 // ---- one directed link = LDS ring (payload) + 3 registers ------------------
-// Tickets never exceed step_cap (<= 8192 < 2^14: a proposer's ticket grows by
-// at most one per step, DESIGN.md "Encodings"), and commands are a clientId
-// (every proposer ticks once, from ticket 0, so t = 1 in "c<id>.1"), so every
-// message is one 32-bit word:
+// Every message is one 32-bit word:
 //   request   x[13:0] | val[15:14] | kind[17:16]
 //   response  x[13:0] | y[27:14]   | val[29:28] | kind[31:30]
 // The due steps (mod 16) of the queued messages sit in one register as a
@@ -126,6 +136,10 @@ __device__ __forceinline__ uint32_t l_due_count(const Link& L, uint32_t s4) {
   const uint32_t tz = x ? (uint32_t)__builtin_ctz(x) : 32u;
   return min(tz >> 2, l_len(L));
 }
+__device__ __forceinline__ void l_pop(Link& L) {
+  L.dn >>= 4;
+  L.hl = (L.hl & ~0x7Fu) | ((L.hl + 1u) & 7u) | ((l_len(L) - 1u) << 3);
+}
 
 template <int PM, int N>
 struct Lds {
@@ -144,6 +158,7 @@ template <> struct Occ<3> { static constexpr int waves = PXB_OCC_P3; };
 template <int PM, int N>
 __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KParams kp) {
   constexpr int G = 64 / N;
+  constexpr uint32_t NM = (1u << N) - 1u;     // slot-local lane mask
   __shared__ Lds<PM, N> s_lds[WPB];
 
   const int lane = threadIdx.x & 63;
@@ -153,51 +168,42 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
   const int a = lane - g * N;
   const bool used = g < G;
   const int base = g * N;
-  const uint64_t gmask = used ? ((((1ull << N) - 1ull)) << base) : 0ull;
-  const uint64_t below = (1ull << base) - 1ull;      // base <= 63
+  const uint32_t ltm = (1u << a) - 1u;        // slot-local lanes below me
   uint32_t* clog = &L.clog[used ? g : 0][0];
   for (int k = lane; k < G * (LT + 1); k += 64) (&L.clog[0][0])[k] = 0u;   // epoch 0 = empty
+  // a ballot restricted to my slot, as an N-bit mask indexed by acceptor
+  auto slot = [&](uint64_t b) -> uint32_t { return used ? ((uint32_t)(b >> base) & NM) : 0u; };
 
-  const uint64_t wave = (uint64_t)blockIdx.x * WPB + wib;
-  const uint64_t nwaves = (uint64_t)gridDim.x * WPB;
-  const uint64_t n = kp.n_instances;
-  uint64_t next = n * wave / nwaves;
-  const uint64_t first_idx = next;
-  const uint64_t end = n * (wave + 1) / nwaves;
+  const uint32_t wave = blockIdx.x * WPB + wib;
+  const uint32_t nwaves = gridDim.x * WPB;
+  const uint32_t n = kp.n_instances;
+  uint32_t next = (uint32_t)((uint64_t)n * wave / nwaves);
+  const uint32_t first_idx = next;
+  const uint32_t end = (uint32_t)((uint64_t)n * (wave + 1) / nwaves);
   const uint32_t k0 = kp.k0, k1 = kp.k1;
 
-  // ---- slot / instance state (slot-uniform unless marked "lane") ----
+  // ---- slot state (replicated in the slot's lanes unless marked "lane") ----
   bool active = false;
-  uint64_t idx = 0;
-  uint32_t ilo = 0, ihi = 0;
-  int32_t s = 0;
-  uint32_t P = 0;
-  uint64_t loss_thr = 0;
-  uint32_t delay_max = 1;
-  bool faulty = false;
-  int32_t skew[PM];
+  uint32_t P = 0, dmax = 1;
+  bool faulty = false, lossy = false, tovf = false;
   int32_t last_tick = 0;
+  int32_t s = 0;                          // current step
+  uint32_t idx = 0;                       // local instance index
+  uint32_t loss_m1 = 0;
+  uint32_t rounds = 0, dval = 0;          // dval: decided clientId (0 = none)
+  int32_t dtick = 0;
   int32_t c0 = 0, c1 = 0;                 // lane: isolation window of acceptor a
   AccState A{0, 0, 0, false};             // lane: acceptor a (ServerState)
-  uint32_t log_len = 0, digest = 0;       // lane
+  uint32_t log_len = 0, lflags = 0, digest = 0;   // lane
   PropState S[PM];                        // replicated proposers (ClientState)
+  int32_t skew[PM];
   Link R[PM], Sx[PM];                     // lane: links p -> a, a -> p
-  uint32_t lflags = 0;                    // lane-local flag bits
-  uint32_t tflags = 0;                    // replicated flag bits
-  uint32_t rounds = 0, dval = 0;
-  int32_t dtick = 0;
-  bool decided = false;
   uint32_t msgs_acc = 0;                  // lane totals across instances
   uint64_t canon_acc = 0;
-  uint32_t rounds_acc = 0, steps_acc = 0; // slot leaders
-  uint32_t wc[PXB_NCOUNTERS];             // wave-uniform counts (ballot + popcount)
-#pragma unroll
-  for (int i = 0; i < PXB_NCOUNTERS; ++i) wc[i] = 0;
-  uint32_t tag = 0;                       // canonical-log epoch of the slot's instance
 #pragma unroll
   for (int p = 0; p < PM; ++p) {
-    skew[p] = 0;
     S[p] = PropState{0, 0, 0, IDLE, 0, 0, 0, 0, false};
+    skew[p] = 0;
     R[p] = Link{0, 0, 0};
     Sx[p] = Link{0, 0, 0};
   }
@@ -210,9 +216,10 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
     int32_t d = 1;
     bool ok = true;
     if (faulty) {
-      const uint4 w = philox(ilo, ihi, k, (1u << 24) | dirbits | (uint32_t)a, k0, k1);
-      ok = (uint64_t)w.x >= loss_thr;
-      d = 1 + (int32_t)mulhi_n(w.y, delay_max);
+      const uint64_t inst = kp.first_instance + idx;
+      const uint4 w = philox((uint32_t)inst, (uint32_t)(inst >> 32), k, (1u << 24) | dirbits | (uint32_t)a, k0, k1);
+      ok = !(lossy && w.x <= loss_m1);
+      d = 1 + (int32_t)mulhi_n(w.y, dmax);
     }
     const uint32_t len = l_len(Lk);
     const bool full = len >= (uint32_t)QD;
@@ -223,22 +230,16 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
     Lk.dn = push ? (Lk.dn | (((uint32_t)due & 15u) << (4u * len))) : Lk.dn;
     Lk.hl = push ? ((Lk.hl & 7u) | ((len + 1u) << 3) | ((uint32_t)due << 8)) : Lk.hl;
   };
-  auto link_pop = [&](Link& Lk) {
-    Lk.dn >>= 4;
-    Lk.hl = (Lk.hl & ~0x7Fu) | ((Lk.hl + 1u) & 7u) | ((l_len(Lk) - 1u) << 3);
-  };
   // proposer p's broadcast copy on link p -> a (sendToAllServers, Client.hs:122-123)
   auto send_req = [&](auto pc, bool has, uint32_t kind, int32_t x, uint32_t z) {
     constexpr int p = decltype(pc)::value;
     if (!has) return;
-    if (kind == ASK) rounds++;
-    if (kind == EXECUTE && !decided) {
-      decided = true;
+    rounds += (kind == ASK) ? 1u : 0u;
+    if (kind == EXECUTE && dval == 0u) {   // first Execute: the decided value
       dval = S[p].r2_v;
       dtick = x;
     }
-    link_send(R[p], &L.rq[p][0][0], (uint32_t)p << 8,
-              ((uint32_t)x & 0x3FFFu) | (z << 14) | (kind << 16));
+    link_send(R[p], &L.rq[p][0][0], (uint32_t)p << 8, ((uint32_t)x & 0x3FFFu) | (z << 14) | (kind << 16));
   };
 
   STAMP_DECL
@@ -246,29 +247,31 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
     // ---------------- refill free slots from this wave's range -------------
     const uint64_t freeb = __ballot(used && !active && a == 0);
     if (freeb != 0ull && next < end) {
-      const uint64_t cand = next + (uint64_t)__popcll(freeb & below);
+      const uint32_t cand = next + (uint32_t)__popcll(freeb & ((1ull << base) - 1ull));
       if (used && !active && cand < end) {
         idx = cand;
         const uint64_t inst = kp.first_instance + cand;
-        ilo = (uint32_t)inst;
-        ihi = (uint32_t)(inst >> 32);
+        const uint32_t ilo = (uint32_t)inst, ihi = (uint32_t)(inst >> 32);
         P = kp.n_prop;
-        uint32_t dmax = kp.delay_max, cppm = kp.crash_ppm;
-        loss_thr = kp.loss_thr;
-        uint64_t crash_thr = kp.crash_thr;
-        if (kp.randomize) {                      // SEMANTICS §4 (config-5 fuzz)
+        dmax = kp.delay_max;
+        lossy = (kp.cfg & CFG_LOSSY) != 0u;
+        bool crashy = (kp.cfg & CFG_CRASHY) != 0u;
+        loss_m1 = kp.loss_m1;
+        uint32_t crash_m1 = kp.crash_m1;
+        if (kp.cfg & CFG_RANDOMIZE) {                  // SEMANTICS §4 (config-5 fuzz)
           const uint4 w = philox(ilo, ihi, 0u, 4u << 24, k0, k1);
           P = 1u + mulhi_n(w.x, kp.n_prop);
-          loss_thr = prob_threshold(mulhi_n(w.y, kp.loss_ppm + 1u));
+          const uint64_t lt = prob_threshold(mulhi_n(w.y, kp.loss_ppm + 1u));
           dmax = 1u + mulhi_n(w.z, kp.delay_max);
-          cppm = mulhi_n(w.w, kp.crash_ppm + 1u);
-          crash_thr = prob_threshold(cppm);
+          const uint64_t ct = prob_threshold(mulhi_n(w.w, kp.crash_ppm + 1u));
+          lossy = lt != 0ull;
+          loss_m1 = (uint32_t)(lt - 1ull);
+          crashy = ct != 0ull;
+          crash_m1 = (uint32_t)(ct - 1ull);
         }
-        delay_max = dmax;
-        faulty = (loss_thr > 0) || (dmax > 1u);
-        last_tick = 0;
         uint4 wsk = make_uint4(0, 0, 0, 0);
         if (kp.skew_max > 0u) wsk = philox(ilo, ihi, 0u, 2u << 24, k0, k1);
+        last_tick = 0;
         static_for<0, PM>([&](auto pc) {
           constexpr int p = decltype(pc)::value;
           const uint32_t wp = (p == 0) ? wsk.x : (p == 1) ? wsk.y : wsk.z;
@@ -279,25 +282,24 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
           Sx[p] = Link{0, 0, 0};
         });
         c0 = c1 = 0;
-        if (cppm > 0u) {
+        if (crashy) {
           const uint4 w = philox(ilo, ihi, 0u, (3u << 24) | (uint32_t)a, k0, k1);
-          if ((uint64_t)w.x < crash_thr) {
+          if (w.x <= crash_m1) {
             c0 = (int32_t)mulhi_n(w.y, kp.crash_start_max + 1u);
             c1 = c0 + 1 + (int32_t)mulhi_n(w.z, kp.crash_len_max);
           }
         }
+        faulty = lossy || dmax > 1u;
+        tovf = false;
         A = AccState{0, 0, 0, false};
-        log_len = 0;
+        log_len = lflags = 0;
         digest = 0x811C9DC5u;
-        lflags = tflags = 0;
         rounds = dval = 0;
         dtick = 0;
-        decided = false;
         s = 0;
-        tag = (uint32_t)(cand - first_idx) + 1u;
         active = true;
       }
-      next = min(next + (uint64_t)__popcll(freeb), end);
+      next = min(next + (uint32_t)__popcll(freeb), end);
     }
     if (!__any(active)) break;
     STAMP(0);
@@ -306,7 +308,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
     // ---------------- acceptor phase: (proposer index, link seq) order -------
     // handleClientRequest, Server.hs:51-78, for every due request of lane a
     {
-      const bool iso = (c0 <= s) && (s < c1);
+      const bool isolated = (c0 <= s) && (s < c1);
       static_for<0, PM>([&](auto pc) {
         constexpr int p = decltype(pc)::value;
         for (;;) {
@@ -314,24 +316,24 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
           if (!__any(due)) break;
           if (due) {
             const uint32_t w = L.rq[p][l_head(R[p])][lane];
-            link_pop(R[p]);
+            l_pop(R[p]);
             const uint32_t kind = (w >> 16) & 3u;
             const uint32_t rb = (kind == PROPOSE) ? 12u : 8u;
-            if (A.dead || iso) {
-              canon_acc += rb;                         // written, discarded
-            } else {
-              canon_acc += 2u * rb + 32u;
+            const bool live = !A.dead && !isolated;
+            canon_acc += live ? 2u * rb + 32u : rb;        // discarded: written, not read
+            if (live) {
               int32_t rx, ry;
               uint32_t rz, ev;
               const uint32_t rk = acceptor_step(A, kind, (int32_t)(w & 0x3FFFu), (w >> 14) & 3u,
                                                 rx, ry, rz, ev);
-              if (A.dead) lflags |= PXB_F_PANIC;
+              lflags |= A.dead ? (uint32_t)PXB_F_PANIC : 0u;
               if (ev != 0u) {
                 digest = fnv_u32(digest, (ev << 24) | 1u);
                 if (log_len < (uint32_t)LT) {
                   // two acceptors of this instance executed different commands at
                   // the same position iff the max already holds this epoch with
                   // another command (order-independent, SEMANTICS §7)
+                  const uint32_t tag = idx - first_idx + 1u;
                   const uint32_t old = atomicMax(&clog[log_len], (tag << 2) | ev);
                   if ((old >> 2) == tag && (old & 3u) != ev) lflags |= PXB_F_LOG_DIVERGENCE;
                 } else {
@@ -347,8 +349,8 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
         }
       });
     }
-
     STAMP(1);
+
     // ---------------- proposer phase: Tick, then (acceptor, link seq) order --
     static_for<0, PM>([&](auto pc) {
       constexpr int p = decltype(pc)::value;
@@ -359,25 +361,27 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
         Req o0{NONE, 0, 0};
         uint32_t no = 0;
         if (tick) {
-          no = proposer_tick(S[p], (uint32_t)(p + 1), o0);   // compact cmd = clientId
+          no = proposer_tick(S[p], (uint32_t)(p + 1), o0);   // compact cmd = clientId (t = 1)
           stepped = true;
         }
         send_req(pc, no > 0u, o0.kind, o0.x, o0.z);
       }
       const uint32_t cnt_p = pact ? l_due_count(Sx[p], s4) : 0u;
       const uint64_t anyb = __ballot(cnt_p > 0u);
+      STAMP(2);
       if (anyb != 0ull) {
-        stepped = stepped || ((anyb & gmask) != 0ull);
-        const uint64_t multi = __ballot(cnt_p > 1u);
-        const bool slot_serial = (multi & gmask) != 0ull;
+        const uint32_t mine_slot = slot(anyb);
+        stepped = stepped || mine_slot != 0u;
+        const bool slot_serial = slot(__ballot(cnt_p > 1u)) != 0u;
         // ---- fast path: every link a -> p of the slot has <= 1 due response.
         // The serial fold of Client.hs:125-189 over acceptors 0..N-1 is done in
         // rounds, one per state-changing event (majority or NACK):
         // acks = __ballot + popcount, the majority acceptor = the lane whose
         // prefix popcount hits the quorum, MostRecent (Common.hs:61-65) = a
-        // slot max-reduction of (t_store, -lane) over the counted acks.
-        const bool fast = pact && !slot_serial && ((anyb & gmask) != 0ull);
-        STAMP(2);
+        // slot max-reduction of (t_store, -lane) over the counted acks.  After
+        // an event only a NACK (not Idle) or a stale Round2Success (in Round2)
+        // can still act: a fresh Round1OK for the new ticket cannot exist yet.
+        const bool fast = pact && !slot_serial && mine_slot != 0u;
         if (__any(fast)) {
           const bool has = fast && cnt_p == 1u;
           const uint32_t w = has ? L.sq[p][l_head(Sx[p])][lane] : 0u;
@@ -385,66 +389,64 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
           const int32_t x = (int32_t)(w & 0x3FFFu);
           const int32_t y = (int32_t)((w >> 14) & 0x3FFFu);
           const uint32_t z = (w >> 28) & 3u;
-          const uint64_t lt = (1ull << lane) - 1ull;
-          uint64_t rem = __ballot(has) & gmask;   // slot's unprocessed responses
+          uint32_t rem = slot(__ballot(has));                 // unprocessed responses
+          const uint32_t havem = slot(__ballot(has && kind == HAVE));
+          const uint32_t r2sm = slot(__ballot(has && kind == R2S));
           bool go = fast;
           while (__any(go)) {
-            const uint32_t rs = S[p].rs;
-            const int32_t T = S[p].ticket;
-            const bool mine = go && ((rem >> lane) & 1ull) != 0ull;
+            PropState& Sp = S[p];
+            const uint32_t rs = Sp.rs;
+            const int32_t T = Sp.ticket;
+            const bool mine = go && ((rem >> a) & 1u) != 0u;
             const bool is_ack = mine && ((rs == ROUND1 && kind == R1OK && x == T) ||
                                          (rs == ROUND2 && kind == R2S));
             const bool is_ab = mine && rs != IDLE && kind == HAVE && x >= T;
-            const uint64_t ackm = __ballot(is_ack) & gmask;
-            const uint64_t abm = __ballot(is_ab) & gmask;
-            const uint32_t need = (uint32_t)(N >> 1) + 1u - S[p].acks;
-            const bool is_maj = is_ack && (uint32_t)__popcll(ackm & lt) + 1u == need;
-            const uint64_t majm = __ballot(is_maj) & gmask;
-            const int e_ab = abm ? __builtin_ctzll(abm) : 64;
-            const int e_mj = majm ? __builtin_ctzll(majm) : 64;
-            const int e = min(e_ab, e_mj);
-            const uint64_t below_e = (e >= 64) ? ~0ull : ((1ull << e) - 1ull);
-            const uint64_t counted = (ackm & below_e) | ((e_mj < e_ab) ? (1ull << e_mj) : 0ull);
+            const uint32_t ackm = slot(__ballot(is_ack));
+            const uint32_t abm = slot(__ballot(is_ab));
+            const uint32_t need = (uint32_t)(N >> 1) + 1u - Sp.acks;
+            const bool is_maj = is_ack && (uint32_t)__popc(ackm & ltm) + 1u == need;
+            const uint32_t majm = slot(__ballot(is_maj));
+            const uint32_t e_ab = abm ? (uint32_t)__builtin_ctz(abm) : 32u;
+            const uint32_t e_mj = majm ? (uint32_t)__builtin_ctz(majm) : 32u;
+            const uint32_t e = min(e_ab, e_mj);
+            const uint32_t below_e = (e >= 32u) ? ~0u : ((1u << e) - 1u);
+            const uint32_t counted = (ackm & below_e) | ((e_mj < e_ab) ? (1u << e_mj) : 0u);
             // MostRecent over the counted Round1OKs that carry a proposal
-            const bool elig = rs == ROUND1 && ((counted >> lane) & 1ull) != 0ull && z != 0u;
-            const uint64_t zb = __ballot(elig) & gmask;
+            const bool elig = rs == ROUND1 && ((counted >> a) & 1u) != 0u && z != 0u;
+            const uint32_t zb = slot(__ballot(elig));
             uint32_t key = elig ? (((uint32_t)y << 5) | (31u - (uint32_t)a)) : 0u;
             uint32_t bz = 0;
-            if (__any(zb != 0ull)) {            // some slot saw a stored proposal
-              if (__any(__popcll(zb) > 1)) {
+            if (__any(zb != 0u)) {              // some slot saw a stored proposal
+              if (__any(__popc(zb) > 1)) {
 #pragma unroll
                 for (int off = 1; off < N; off <<= 1) {
                   const uint32_t o = (uint32_t)__shfl((int)key, lane + off);
                   if (a + off < N) key = max(key, o);
                 }
               }
-              const int src = zb ? ((__popcll(zb) > 1) ? base : __builtin_ctzll(zb)) : lane;
+              const int src = zb ? ((__popc(zb) > 1) ? base : base + __builtin_ctz(zb)) : lane;
               key = (uint32_t)__shfl((int)key, src);
-              const int wl = base + 31 - (int)(key & 31u);
-              bz = (uint32_t)__shfl((int)z, zb ? wl : lane);
+              bz = (uint32_t)__shfl((int)z, zb ? base + 31 - (int)(key & 31u) : lane);
             }
             uint32_t u = 0;
-            if (__any(abm != 0ull)) u = (uint32_t)__shfl(x, e_ab < 64 ? e_ab : lane);
+            if (__any(abm != 0u)) u = (uint32_t)__shfl(x, e_ab < 32u ? base + (int)e_ab : lane);
             Req o0{NONE, 0, 0}, o1{NONE, 0, 0};
             uint32_t no = 0;
             if (go) {
-              PropState& Sp = S[p];
               int32_t mt = Sp.mr_t;
               uint32_t mv = Sp.mr_v;
-              if (zb != 0ull && (mv == 0u || (int32_t)(key >> 5) > mt)) {
+              if (zb != 0u && (mv == 0u || (int32_t)(key >> 5) > mt)) {
                 mt = (int32_t)(key >> 5);
                 mv = bz;
               }
-              Sp.acks += (uint32_t)__popcll(counted);
-              if (e >= 64) {                       // no event: only acks
+              Sp.acks += (uint32_t)__popc(counted);
+              if (e >= 32u) {                      // no event: only acks
                 if (rs == ROUND1) {
                   Sp.mr_t = mt;
                   Sp.mr_v = mv;
                 }
-                go = false;
-              } else if (e_mj < e_ab) {            // majority reached at lane e
+              } else if (e_mj < e_ab) {            // majority reached at acceptor e
                 if (rs == ROUND1) {                // Client.hs:157-170
-                  Sp.r2_t = T;
                   Sp.r2_v = (mv == 0u) ? Sp.cmd : mv;
                   Sp.pending = (mv != 0u);
                   Sp.acks = 0;
@@ -479,10 +481,8 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
                 o0 = Req{ASK, (int32_t)u + 1, 0};
                 no = 1;
               }
-              if (e < 64) {
-                rem &= ~(below_e | (1ull << e));
-                if (rem == 0ull) go = false;
-              }
+              rem &= (e >= 32u) ? 0u : ~(below_e | (1u << e));
+              go = Sp.rs != IDLE && (rem & (havem | (Sp.rs == ROUND2 ? r2sm : 0u))) != 0u;
             }
 #pragma unroll 1
             for (uint32_t k = 0; k < 2u; ++k) {
@@ -492,13 +492,13 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
           }
           if (has) {
             canon_acc += 2u * (16u >> kind);
-            link_pop(Sx[p]);
+            l_pop(Sx[p]);
           }
         }
+        STAMP(3);
         // ---- general path (a link holds >= 2 due responses): serial fold in
         // canonical order; every lane of the slot reads the head of lane aa's
         // link (ds_bpermute) and applies handleServerResponse; lane aa pops it.
-        STAMP(3);
         const uint32_t cnt_s = slot_serial ? cnt_p : 0u;
         if (__any(cnt_s > 0u)) {
 #pragma unroll 1
@@ -516,7 +516,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
                                    (int32_t)((w >> 14) & 0x3FFFu), (w >> 28) & 3u, o0, o1);
                 if (a == aa) {
                   canon_acc += 2u * (16u >> kind);
-                  link_pop(Sx[p]);
+                  l_pop(Sx[p]);
                 }
                 ca--;
               }
@@ -529,69 +529,53 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
           }
         }
       }
-      if (stepped && a == 0) canon_acc += 48u;
-      if (pact && S[p].ticket >= PXB_TICKET_LIMIT) tflags |= PXB_F_TICKET_OVERFLOW;
+      canon_acc += (stepped && a == 0) ? 48u : 0u;
+      tovf = tovf || (pact && S[p].ticket >= PXB_TICKET_LIMIT);
     });
-
     STAMP(4);
+
     // ---------------- end of step: quiescence / step cap ---------------------
-    bool busy = false;
+    uint32_t lens = 0;
 #pragma unroll
-    for (int p = 0; p < PM; ++p) busy = busy || ((R[p].hl | Sx[p].hl) & 0x78u) != 0u;
-    const uint64_t busyb = __ballot(active && busy);
-    const bool quiet = active && ((busyb & gmask) == 0ull) && s >= last_tick;
+    for (int p = 0; p < PM; ++p) lens |= R[p].hl | Sx[p].hl;
+    const uint64_t busyb = __ballot(active && (lens & 0x78u) != 0u);
+    const bool quiet = active && slot(busyb) == 0u && s >= last_tick;
     const bool cap = active && !quiet && (s + 1 >= (int32_t)kp.step_cap);
-    if (active) s++;
+    s += active ? 1 : 0;
     const bool done = quiet || cap;
     if (__any(done)) {
-      const uint64_t pan = __ballot((lflags & PXB_F_PANIC) != 0u);
-      const uint64_t dvg = __ballot((lflags & PXB_F_LOG_DIVERGENCE) != 0u);
-      const uint64_t qov = __ballot((lflags & PXB_F_QUEUE_OVERFLOW) != 0u);
-      const uint64_t trc = __ballot((lflags & PXB_F_LOG_TRUNC) != 0u);
-      uint32_t f = tflags;
-      f |= (pan & gmask) ? (uint32_t)PXB_F_PANIC : 0u;
-      f |= (dvg & gmask) ? (uint32_t)PXB_F_LOG_DIVERGENCE : 0u;
-      f |= (qov & gmask) ? (uint32_t)PXB_F_QUEUE_OVERFLOW : 0u;
-      f |= (trc & gmask) ? (uint32_t)PXB_F_LOG_TRUNC : 0u;
-      f |= cap ? (uint32_t)PXB_F_STEP_CAP : 0u;
-      f |= decided ? 0u : (uint32_t)PXB_F_UNDECIDED;
-#pragma unroll
-      for (int p = 0; p < PM; ++p)
-        f |= (!cap && (uint32_t)p < P && S[p].rs != IDLE) ? (uint32_t)PXB_F_STUCK : 0u;
-      const bool lead = done && a == 0;
-      // run totals: one ballot + popcount per counter over the finishing slots
-      wc[PXB_C_INSTANCES] += (uint32_t)__popcll(__ballot(lead));
-      wc[PXB_C_UNDECIDED] += (uint32_t)__popcll(__ballot(lead && (f & PXB_F_UNDECIDED)));
-      if (__any(lead && (f & ~(uint32_t)PXB_F_UNDECIDED) != 0u)) {
-        wc[PXB_C_STUCK] += (uint32_t)__popcll(__ballot(lead && (f & PXB_F_STUCK)));
-        wc[PXB_C_PANIC] += (uint32_t)__popcll(__ballot(lead && (f & PXB_F_PANIC)));
-        wc[PXB_C_DIVERGENCE] += (uint32_t)__popcll(__ballot(lead && (f & PXB_F_LOG_DIVERGENCE)));
-        wc[PXB_C_STEP_CAP] += (uint32_t)__popcll(__ballot(lead && (f & PXB_F_STEP_CAP)));
-        wc[PXB_C_QUEUE_OVERFLOW] += (uint32_t)__popcll(__ballot(lead && (f & PXB_F_QUEUE_OVERFLOW)));
-        wc[PXB_C_TICKET_OVERFLOW] += (uint32_t)__popcll(__ballot(lead && (f & PXB_F_TICKET_OVERFLOW)));
-        wc[PXB_C_LOG_TRUNC] += (uint32_t)__popcll(__ballot(lead && (f & PXB_F_LOG_TRUNC)));
-      }
+      const uint32_t pan = slot(__ballot((lflags & PXB_F_PANIC) != 0u));
+      const uint32_t dvg = slot(__ballot((lflags & PXB_F_LOG_DIVERGENCE) != 0u));
+      const uint32_t qov = slot(__ballot((lflags & PXB_F_QUEUE_OVERFLOW) != 0u));
+      const uint32_t trc = slot(__ballot((lflags & PXB_F_LOG_TRUNC) != 0u));
       if (done) {
-        const uint32_t steps = (uint32_t)s;
-        rounds_acc += lead ? rounds : 0u;
-        steps_acc += lead ? steps : 0u;
-        canon_acc += lead ? 20u : 4u;                 // result record + this digest
-        if (lead && kp.out) {
+        uint32_t f = tovf ? (uint32_t)PXB_F_TICKET_OVERFLOW : 0u;
+        f |= pan ? (uint32_t)PXB_F_PANIC : 0u;
+        f |= dvg ? (uint32_t)PXB_F_LOG_DIVERGENCE : 0u;
+        f |= qov ? (uint32_t)PXB_F_QUEUE_OVERFLOW : 0u;
+        f |= trc ? (uint32_t)PXB_F_LOG_TRUNC : 0u;
+        f |= cap ? (uint32_t)PXB_F_STEP_CAP : 0u;
+        f |= dval ? 0u : (uint32_t)PXB_F_UNDECIDED;
+#pragma unroll
+        for (int p = 0; p < PM; ++p)
+          f |= (!cap && (uint32_t)p < P && S[p].rs != IDLE) ? (uint32_t)PXB_F_STUCK : 0u;
+        canon_acc += (a == 0) ? 20u : 4u;          // result record + this digest
+        if (a == 0) {
           uint4 r;
-          r.x = decided ? ((dval << 24) | 1u) : 0u;
-          r.y = decided ? (uint32_t)dtick : 0u;
+          r.x = dval ? ((dval << 24) | 1u) : 0u;
+          r.y = dval ? (uint32_t)dtick : 0u;
           r.z = rounds;
-          r.w = (f & 0xFFu) | (min(steps, 0xFFFFu) << 16);
-          *reinterpret_cast<uint4*>(kp.out + idx) = r;
+          r.w = (f & 0xFFu) | ((uint32_t)s << 16);
+          kp.out[idx] = r;
         }
-        if (kp.dig) kp.dig[idx * N + a] = fnv_u32(digest, log_len);
+        if (kp.dig) kp.dig[(uint64_t)idx * N + a] = fnv_u32(digest, log_len);
         if (kp.acc) {
           uint4 r;
           r.x = (uint32_t)A.t_max;
           r.y = (uint32_t)A.t_store;
           r.z = A.val ? ((A.val << 24) | 1u) : 0u;
           r.w = log_len | ((A.dead ? 1u : 0u) << 31);
-          *reinterpret_cast<uint4*>(kp.acc + idx * N + a) = r;
+          kp.acc[(uint64_t)idx * N + a] = r;
         }
         active = false;
       }
@@ -601,28 +585,72 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
 
   STAMP(6);
   STAMP_FLUSH(kp.dbg);
-  // ---------------- flush wave totals -----------------------------------------
-  uint32_t m = msgs_acc, ra = rounds_acc, sa = steps_acc;
+  // ---------------- flush lane totals (messages, canonical bytes) ------------
+  uint32_t m = msgs_acc;
   uint64_t c64 = canon_acc;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     m += (uint32_t)__shfl_xor((int)m, off);
-    ra += (uint32_t)__shfl_xor((int)ra, off);
-    sa += (uint32_t)__shfl_xor((int)sa, off);
     const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)c64, off);
     const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(c64 >> 32), off);
     c64 += ((uint64_t)hi << 32) | lo;
   }
-  wc[PXB_C_DECIDED] = wc[PXB_C_INSTANCES] - wc[PXB_C_UNDECIDED];
   if (lane == 0) {
-    unsigned long long* T = kp.totals;
-    atomicAdd(&T[PXB_C_MESSAGES], (unsigned long long)m);
-    atomicAdd(&T[PXB_C_CANON_BYTES], (unsigned long long)c64);
-    atomicAdd(&T[PXB_C_ROUNDS], (unsigned long long)ra);
-    atomicAdd(&T[PXB_C_STEPS], (unsigned long long)sa);
+    atomicAdd(&kp.totals[PXB_C_MESSAGES], (unsigned long long)m);
+    atomicAdd(&kp.totals[PXB_C_CANON_BYTES], (unsigned long long)c64);
+  }
+}
+
+// ---- run totals from the result records ---------------------------------------
+// (decided / undecided / flag counts / rounds / steps / instances)
+constexpr int RED_BLOCK = 256;
+__global__ __launch_bounds__(RED_BLOCK) void reduce_results_kernel(const uint4* __restrict__ res, uint32_t n,
+                                                                   unsigned long long* totals) {
+  // per-thread partial counts: [0] instances [1] undecided [2] stuck [3] panic
+  // [4] divergence [5] step_cap [6] rounds [7] steps [8] qovf [9] tovf [10] trunc
+  uint32_t c[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (uint32_t i = blockIdx.x * RED_BLOCK + threadIdx.x; i < n; i += gridDim.x * RED_BLOCK) {
+    const uint4 r = res[i];
+    const uint32_t f = r.w;
+    c[0] += 1u;
+    c[1] += f & 1u;
+    c[2] += (f >> 1) & 1u;
+    c[3] += (f >> 2) & 1u;
+    c[4] += (f >> 3) & 1u;
+    c[5] += (f >> 4) & 1u;
+    c[8] += (f >> 5) & 1u;
+    c[9] += (f >> 6) & 1u;
+    c[10] += (f >> 7) & 1u;
+    c[6] += r.z;
+    c[7] += f >> 16;
+  }
+  __shared__ uint32_t part[RED_BLOCK / 64][11];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
-    for (int i = 0; i < PXB_NCOUNTERS; ++i)
-      if (wc[i] != 0u) atomicAdd(&T[i], (unsigned long long)wc[i]);
+  for (int k = 0; k < 11; ++k) {
+    uint32_t v = c[k];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += (uint32_t)__shfl_xor((int)v, off);
+    if (lane == 0) part[w][k] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 11) {
+    unsigned long long v = 0;
+#pragma unroll
+    for (int q = 0; q < RED_BLOCK / 64; ++q) v += part[q][threadIdx.x];
+    const int slot[11] = {PXB_C_INSTANCES, PXB_C_UNDECIDED, PXB_C_STUCK, PXB_C_PANIC,
+                          PXB_C_DIVERGENCE, PXB_C_STEP_CAP, PXB_C_ROUNDS, PXB_C_STEPS,
+                          PXB_C_QUEUE_OVERFLOW, PXB_C_TICKET_OVERFLOW, PXB_C_LOG_TRUNC};
+    if (v) atomicAdd(&totals[slot[threadIdx.x]], v);
+  }
+  if (threadIdx.x == 0) {
+    unsigned long long inst = 0, und = 0;
+#pragma unroll
+    for (int q = 0; q < RED_BLOCK / 64; ++q) {
+      inst += part[q][0];
+      und += part[q][1];
+    }
+    if (inst - und) atomicAdd(&totals[PXB_C_DECIDED], inst - und);
   }
 }
 
@@ -700,6 +728,8 @@ static unsigned long long* g_dbg = nullptr;
 static std::mutex g_mu;
 static int g_occ[4][10][64];            // [pm][n][device] blocks per CU (0 = unknown)
 static int g_cus[64];
+static void* g_scratch[64];             // per device: result records when the caller passes none
+static size_t g_scratch_bytes[64];
 
 static int hip_fail(hipError_t e) {
   g_last_hip = (int)e;
@@ -769,7 +799,12 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
   if (dev < 0 || dev >= 64) return PXB_E_NODEV;
   kernel_fn fn = pick(cfg->n_proposers, cfg->n_acceptors);
   if (!fn) return PXB_E_INVAL;
+  const hipStream_t st = (hipStream_t)stream;
+  // without caller-provided result records the run goes through a cached
+  // scratch buffer in chunks (the totals are reduced from those records)
+  const uint64_t chunk_max = d_out ? (1ull << 31) : (1ull << 24);
   int occ, cus;
+  uint4* scratch = nullptr;
   {
     std::lock_guard<std::mutex> lk(g_mu);
     if (!g_cus[dev]) {
@@ -785,27 +820,36 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
     }
     occ = o;
     cus = g_cus[dev];
+    static const char* cap_env = getenv("PXB_BLOCKS_PER_CU");   // experiments: cap residency
+    if (cap_env && atoi(cap_env) > 0) occ = std::min(occ, atoi(cap_env));
+    if (!d_out) {
+      const size_t need = (size_t)std::min<uint64_t>(cfg->n_instances, chunk_max) * sizeof(uint4);
+      if (g_scratch_bytes[dev] < need) {
+        if (g_scratch[dev]) (void)hipFree(g_scratch[dev]);
+        g_scratch[dev] = nullptr;
+        g_scratch_bytes[dev] = 0;
+        HIPCHK(hipMalloc(&g_scratch[dev], need));
+        g_scratch_bytes[dev] = need;
+      }
+      scratch = (uint4*)g_scratch[dev];
+    }
   }
   KParams kp;
   memset(&kp, 0, sizeof(kp));
-  kp.first_instance = cfg->first_instance;
-  kp.n_instances = cfg->n_instances;
   kp.k0 = (uint32_t)cfg->seed;
   kp.k1 = (uint32_t)(cfg->seed >> 32);
   kp.n_prop = cfg->n_proposers;
-  kp.loss_ppm = cfg->loss_ppm;
   kp.delay_max = cfg->delay_max;
+  kp.loss_ppm = cfg->loss_ppm;
   kp.crash_ppm = cfg->crash_ppm;
   kp.crash_len_max = cfg->crash_len_max;
   kp.crash_start_max = cfg->crash_start_max;
   kp.skew_max = cfg->skew_max;
   kp.step_cap = cfg->step_cap;
-  kp.randomize = (cfg->flags & PXB_CFG_RANDOMIZE) ? 1u : 0u;
-  kp.loss_thr = prob_threshold(cfg->loss_ppm);
-  kp.crash_thr = prob_threshold(cfg->crash_ppm);
-  kp.out = d_out;
-  kp.dig = d_log_digest;
-  kp.acc = d_acc;
+  const uint64_t lt = prob_threshold(cfg->loss_ppm), ct = prob_threshold(cfg->crash_ppm);
+  kp.cfg = ((cfg->flags & PXB_CFG_RANDOMIZE) ? CFG_RANDOMIZE : 0u) | (lt ? CFG_LOSSY : 0u) | (ct ? CFG_CRASHY : 0u);
+  kp.loss_m1 = (uint32_t)(lt - 1ull);
+  kp.crash_m1 = (uint32_t)(ct - 1ull);
   kp.totals = reinterpret_cast<unsigned long long*>(d_totals);
 #ifdef PXB_STAMPS
   {
@@ -819,12 +863,23 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
   }
 #endif
   const uint64_t G = 64 / cfg->n_acceptors;
-  const uint64_t waves_needed = (cfg->n_instances + G - 1) / G;
-  const uint64_t blocks_needed = (waves_needed + WPB - 1) / WPB;
   const uint64_t resident = (uint64_t)occ * (uint64_t)cus;
-  const unsigned grid = (unsigned)std::min<uint64_t>(blocks_needed, resident);
-  hipLaunchKernelGGL(fn, dim3(grid), dim3(BLOCK), 0, (hipStream_t)stream, kp);
-  HIPCHK(hipGetLastError());
+  for (uint64_t done = 0; done < cfg->n_instances; done += chunk_max) {
+    const uint64_t nc = std::min<uint64_t>(chunk_max, cfg->n_instances - done);
+    kp.first_instance = cfg->first_instance + done;
+    kp.n_instances = (uint32_t)nc;
+    kp.out = d_out ? reinterpret_cast<uint4*>(d_out + done) : scratch;
+    kp.dig = d_log_digest ? d_log_digest + done * cfg->n_acceptors : nullptr;
+    kp.acc = d_acc ? reinterpret_cast<uint4*>(d_acc + done * cfg->n_acceptors) : nullptr;
+    const uint64_t waves_needed = (nc + G - 1) / G;
+    const uint64_t blocks_needed = (waves_needed + WPB - 1) / WPB;
+    const unsigned grid = (unsigned)std::min<uint64_t>(blocks_needed, resident);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(BLOCK), 0, st, kp);
+    HIPCHK(hipGetLastError());
+    const unsigned rgrid = (unsigned)std::min<uint64_t>((nc + RED_BLOCK - 1) / RED_BLOCK, (uint64_t)cus * 4);
+    hipLaunchKernelGGL(reduce_results_kernel, dim3(rgrid), dim3(RED_BLOCK), 0, st, kp.out, (uint32_t)nc, kp.totals);
+    HIPCHK(hipGetLastError());
+  }
   return PXB_OK;
 }
 

@@ -8,7 +8,7 @@ from collections import defaultdict
 
 def main(root, kernel_sub="paxos_batch_kernel"):
     agg = defaultdict(list)
-    for f in glob.glob(os.path.join(root, "*", "**", "*counter_collection.csv"), recursive=True):
+    for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 if kernel_sub not in row.get("Kernel_Name", ""):
