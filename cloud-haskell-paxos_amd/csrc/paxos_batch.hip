@@ -85,6 +85,11 @@ __host__ __device__ inline uint64_t prob_threshold(uint32_t ppm) {
   return ((((uint64_t)ppm) << 32) + 999999ull) / 1000000ull;
 }
 
+// wave ballot straight from the lane predicate (HIP's __ballot(int) adds a
+// bool -> int -> compare round trip per call)
+__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+__device__ __forceinline__ bool any(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0ull; }
+
 // compile-time loop: every per-proposer register index is a constant
 template <int I, int E, typename F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -172,7 +177,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
   uint32_t* clog = &L.clog[used ? g : 0][0];
   for (int k = lane; k < G * (LT + 1); k += 64) (&L.clog[0][0])[k] = 0u;   // epoch 0 = empty
   // a ballot restricted to my slot, as an N-bit mask indexed by acceptor
-  auto slot = [&](uint64_t b) -> uint32_t { return used ? ((uint32_t)(b >> base) & NM) : 0u; };
+  auto slot = [&](uint64_t b) -> uint32_t { return (uint32_t)(b >> base) & NM; };   // unused lanes never act
 
   const uint32_t wave = blockIdx.x * WPB + wib;
   const uint32_t nwaves = gridDim.x * WPB;
@@ -245,7 +250,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
   STAMP_DECL
   for (;;) {
     // ---------------- refill free slots from this wave's range -------------
-    const uint64_t freeb = __ballot(used && !active && a == 0);
+    const uint64_t freeb = ballot(used && !active && a == 0);
     if (freeb != 0ull && next < end) {
       const uint32_t cand = next + (uint32_t)__popcll(freeb & ((1ull << base) - 1ull));
       if (used && !active && cand < end) {
@@ -301,7 +306,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
       }
       next = min(next + (uint32_t)__popcll(freeb), end);
     }
-    if (!__any(active)) break;
+    if (!any(active)) break;
     STAMP(0);
 
     const uint32_t s4 = (uint32_t)s & 15u;
@@ -313,7 +318,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
         constexpr int p = decltype(pc)::value;
         for (;;) {
           const bool due = active && l_len(R[p]) > 0u && (R[p].dn & 15u) == s4;
-          if (!__any(due)) break;
+          if (!any(due)) break;
           if (due) {
             const uint32_t w = L.rq[p][l_head(R[p])][lane];
             l_pop(R[p]);
@@ -357,7 +362,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
       const bool pact = active && (uint32_t)p < P;
       bool stepped = false;
       const bool tick = pact && s == skew[p];
-      if (__any(tick)) {                          // handleTick, Client.hs:196-207
+      if (any(tick)) {                          // handleTick, Client.hs:196-207
         Req o0{NONE, 0, 0};
         uint32_t no = 0;
         if (tick) {
@@ -367,12 +372,12 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
         send_req(pc, no > 0u, o0.kind, o0.x, o0.z);
       }
       const uint32_t cnt_p = pact ? l_due_count(Sx[p], s4) : 0u;
-      const uint64_t anyb = __ballot(cnt_p > 0u);
+      const uint64_t anyb = ballot(cnt_p > 0u);
       STAMP(2);
       if (anyb != 0ull) {
         const uint32_t mine_slot = slot(anyb);
         stepped = stepped || mine_slot != 0u;
-        const bool slot_serial = slot(__ballot(cnt_p > 1u)) != 0u;
+        const bool slot_serial = slot(ballot(cnt_p > 1u)) != 0u;
         // ---- fast path: every link a -> p of the slot has <= 1 due response.
         // The serial fold of Client.hs:125-189 over acceptors 0..N-1 is done in
         // rounds, one per state-changing event (majority or NACK):
@@ -382,18 +387,18 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
         // an event only a NACK (not Idle) or a stale Round2Success (in Round2)
         // can still act: a fresh Round1OK for the new ticket cannot exist yet.
         const bool fast = pact && !slot_serial && mine_slot != 0u;
-        if (__any(fast)) {
+        if (any(fast)) {
           const bool has = fast && cnt_p == 1u;
           const uint32_t w = has ? L.sq[p][l_head(Sx[p])][lane] : 0u;
           const uint32_t kind = w >> 30;
           const int32_t x = (int32_t)(w & 0x3FFFu);
           const int32_t y = (int32_t)((w >> 14) & 0x3FFFu);
           const uint32_t z = (w >> 28) & 3u;
-          uint32_t rem = slot(__ballot(has));                 // unprocessed responses
-          const uint32_t havem = slot(__ballot(has && kind == HAVE));
-          const uint32_t r2sm = slot(__ballot(has && kind == R2S));
+          uint32_t rem = slot(ballot(has));                 // unprocessed responses
+          const uint32_t havem = slot(ballot(has && kind == HAVE));
+          const uint32_t r2sm = slot(ballot(has && kind == R2S));
           bool go = fast;
-          while (__any(go)) {
+          while (any(go)) {
             PropState& Sp = S[p];
             const uint32_t rs = Sp.rs;
             const int32_t T = Sp.ticket;
@@ -401,11 +406,11 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
             const bool is_ack = mine && ((rs == ROUND1 && kind == R1OK && x == T) ||
                                          (rs == ROUND2 && kind == R2S));
             const bool is_ab = mine && rs != IDLE && kind == HAVE && x >= T;
-            const uint32_t ackm = slot(__ballot(is_ack));
-            const uint32_t abm = slot(__ballot(is_ab));
+            const uint32_t ackm = slot(ballot(is_ack));
+            const uint32_t abm = slot(ballot(is_ab));
             const uint32_t need = (uint32_t)(N >> 1) + 1u - Sp.acks;
             const bool is_maj = is_ack && (uint32_t)__popc(ackm & ltm) + 1u == need;
-            const uint32_t majm = slot(__ballot(is_maj));
+            const uint32_t majm = slot(ballot(is_maj));
             const uint32_t e_ab = abm ? (uint32_t)__builtin_ctz(abm) : 32u;
             const uint32_t e_mj = majm ? (uint32_t)__builtin_ctz(majm) : 32u;
             const uint32_t e = min(e_ab, e_mj);
@@ -413,11 +418,11 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
             const uint32_t counted = (ackm & below_e) | ((e_mj < e_ab) ? (1u << e_mj) : 0u);
             // MostRecent over the counted Round1OKs that carry a proposal
             const bool elig = rs == ROUND1 && ((counted >> a) & 1u) != 0u && z != 0u;
-            const uint32_t zb = slot(__ballot(elig));
+            const uint32_t zb = slot(ballot(elig));
             uint32_t key = elig ? (((uint32_t)y << 5) | (31u - (uint32_t)a)) : 0u;
             uint32_t bz = 0;
-            if (__any(zb != 0u)) {              // some slot saw a stored proposal
-              if (__any(__popc(zb) > 1)) {
+            if (any(zb != 0u)) {              // some slot saw a stored proposal
+              if (any(__popc(zb) > 1)) {
 #pragma unroll
                 for (int off = 1; off < N; off <<= 1) {
                   const uint32_t o = (uint32_t)__shfl((int)key, lane + off);
@@ -429,7 +434,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
               bz = (uint32_t)__shfl((int)z, zb ? base + 31 - (int)(key & 31u) : lane);
             }
             uint32_t u = 0;
-            if (__any(abm != 0u)) u = (uint32_t)__shfl(x, e_ab < 32u ? base + (int)e_ab : lane);
+            if (any(abm != 0u)) u = (uint32_t)__shfl(x, e_ab < 32u ? base + (int)e_ab : lane);
             Req o0{NONE, 0, 0}, o1{NONE, 0, 0};
             uint32_t no = 0;
             if (go) {
@@ -487,7 +492,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
 #pragma unroll 1
             for (uint32_t k = 0; k < 2u; ++k) {
               const bool hs = no > k;
-              if (__any(hs)) send_req(pc, hs, k ? o1.kind : o0.kind, k ? o1.x : o0.x, k ? o1.z : o0.z);
+              if (any(hs)) send_req(pc, hs, k ? o1.kind : o0.kind, k ? o1.x : o0.x, k ? o1.z : o0.z);
             }
           }
           if (has) {
@@ -500,11 +505,11 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
         // canonical order; every lane of the slot reads the head of lane aa's
         // link (ds_bpermute) and applies handleServerResponse; lane aa pops it.
         const uint32_t cnt_s = slot_serial ? cnt_p : 0u;
-        if (__any(cnt_s > 0u)) {
+        if (any(cnt_s > 0u)) {
 #pragma unroll 1
           for (int aa = 0; aa < N; ++aa) {
             uint32_t ca = (uint32_t)__shfl((int)cnt_s, base + aa);
-            while (__any(ca > 0u)) {
+            while (any(ca > 0u)) {
               const bool take = ca > 0u;
               const uint32_t mine = L.sq[p][l_head(Sx[p])][lane];
               const uint32_t w = (uint32_t)__shfl((int)mine, base + aa);
@@ -523,7 +528,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
 #pragma unroll 1
               for (uint32_t k = 0; k < 2u; ++k) {
                 const bool hs = no > k;
-                if (__any(hs)) send_req(pc, hs, k ? o1.kind : o0.kind, k ? o1.x : o0.x, k ? o1.z : o0.z);
+                if (any(hs)) send_req(pc, hs, k ? o1.kind : o0.kind, k ? o1.x : o0.x, k ? o1.z : o0.z);
               }
             }
           }
@@ -538,16 +543,16 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
     uint32_t lens = 0;
 #pragma unroll
     for (int p = 0; p < PM; ++p) lens |= R[p].hl | Sx[p].hl;
-    const uint64_t busyb = __ballot(active && (lens & 0x78u) != 0u);
+    const uint64_t busyb = ballot(active && (lens & 0x78u) != 0u);
     const bool quiet = active && slot(busyb) == 0u && s >= last_tick;
     const bool cap = active && !quiet && (s + 1 >= (int32_t)kp.step_cap);
     s += active ? 1 : 0;
     const bool done = quiet || cap;
-    if (__any(done)) {
-      const uint32_t pan = slot(__ballot((lflags & PXB_F_PANIC) != 0u));
-      const uint32_t dvg = slot(__ballot((lflags & PXB_F_LOG_DIVERGENCE) != 0u));
-      const uint32_t qov = slot(__ballot((lflags & PXB_F_QUEUE_OVERFLOW) != 0u));
-      const uint32_t trc = slot(__ballot((lflags & PXB_F_LOG_TRUNC) != 0u));
+    if (any(done)) {
+      const uint32_t pan = slot(ballot((lflags & PXB_F_PANIC) != 0u));
+      const uint32_t dvg = slot(ballot((lflags & PXB_F_LOG_DIVERGENCE) != 0u));
+      const uint32_t qov = slot(ballot((lflags & PXB_F_QUEUE_OVERFLOW) != 0u));
+      const uint32_t trc = slot(ballot((lflags & PXB_F_LOG_TRUNC) != 0u));
       if (done) {
         uint32_t f = tovf ? (uint32_t)PXB_F_TICKET_OVERFLOW : 0u;
         f |= pan ? (uint32_t)PXB_F_PANIC : 0u;
