@@ -1,0 +1,155 @@
+{-# LANGUAGE ForeignFunctionInterface #-}
+-- | Haskell binding of the MI355X batched Paxos engine (include/paxos_batch.h).
+--
+-- This is the module a maintainer adds next to the reference's src/Common.hs so
+-- that app/Main.hs (/root/reference/app/Main.hs:27-53) can run batches of the
+-- same single-decree protocol on GPUs instead of spawning Cloud Haskell
+-- processes.  Results come back in the reference's vocabulary: 'Ticket'
+-- (Common.hs:20-22), 'Command' = "c<clientId>.<t>" (Client.hs:202-203) and
+-- 'Proposal' (Common.hs:29-30).
+--
+-- UNVERIFIED: neither this image nor the GPU box has GHC/stack/cabal
+-- (SURVEY.md §8c), so this file has not been compiled.  The C side it binds is
+-- exercised by tests/test_abi.py (symbols, struct layout) and the GPU tests.
+--
+-- The calls are `safe`: a batch blocks for the whole GPU run, and with the
+-- threaded RTS (package.yaml:41-43, -threaded -with-rtsopts=-N) other
+-- capabilities keep running meanwhile.
+module PaxosBatch
+  ( BatchConfig (..)
+  , Outcome (..)
+  , Flag (..)
+  , Totals (..)
+  , defaultConfig
+  , config2
+  , runBatch
+  , runBatchMulti
+  , commandOf
+  ) where
+
+import           Common                (Command, Proposal, Ticket (..))
+
+import           Control.Monad         (forM)
+import           Data.Bits             (shiftR, testBit, (.&.))
+import           Data.Int              (Int32, Int64)
+import           Data.Word             (Word32, Word64)
+import           Foreign.C.String      (CString, peekCString)
+import           Foreign.C.Types       (CInt (..))
+import           Foreign.ForeignPtr    (mallocForeignPtrArray, withForeignPtr)
+import           Foreign.Marshal.Array (advancePtr, allocaArray, peekArray)
+import           Foreign.Marshal.Utils (with)
+import           Foreign.Ptr           (Ptr, nullPtr)
+import           Foreign.Storable      (Storable (..))
+
+-- | pxb_config (64 bytes, see include/paxos_batch.h).
+data BatchConfig = BatchConfig
+  { bcSeed          :: !Word64
+  , bcFirst         :: !Word64   -- ^ global id of the first instance
+  , bcCount         :: !Word64   -- ^ instances in this batch
+  , bcProposers     :: !Word32   -- ^ P, clientIds 1..P  (Main.hs:45 uses 2)
+  , bcAcceptors     :: !Word32   -- ^ N                  (Main.hs:41 uses 2)
+  , bcLossPpm       :: !Word32
+  , bcDelayMax      :: !Word32
+  , bcCrashPpm      :: !Word32
+  , bcCrashLenMax   :: !Word32
+  , bcCrashStartMax :: !Word32
+  , bcSkewMax       :: !Word32
+  , bcStepCap       :: !Word32
+  , bcFlags         :: !Word32
+  } deriving (Show)
+
+instance Storable BatchConfig where
+  sizeOf _ = 64
+  alignment _ = 8
+  peek p = BatchConfig
+    <$> peekByteOff p 0  <*> peekByteOff p 8  <*> peekByteOff p 16
+    <*> peekByteOff p 24 <*> peekByteOff p 28 <*> peekByteOff p 32
+    <*> peekByteOff p 36 <*> peekByteOff p 40 <*> peekByteOff p 44
+    <*> peekByteOff p 48 <*> peekByteOff p 52 <*> peekByteOff p 56
+    <*> peekByteOff p 60
+  poke p c = do
+    pokeByteOff p 0  (bcSeed c);        pokeByteOff p 8  (bcFirst c)
+    pokeByteOff p 16 (bcCount c);       pokeByteOff p 24 (bcProposers c)
+    pokeByteOff p 28 (bcAcceptors c);   pokeByteOff p 32 (bcLossPpm c)
+    pokeByteOff p 36 (bcDelayMax c);    pokeByteOff p 40 (bcCrashPpm c)
+    pokeByteOff p 44 (bcCrashLenMax c); pokeByteOff p 48 (bcCrashStartMax c)
+    pokeByteOff p 52 (bcSkewMax c);     pokeByteOff p 56 (bcStepCap c)
+    pokeByteOff p 60 (bcFlags c)
+
+-- | The stock topology of app/Main.hs (2 acceptors, 2 proposers), fault-free.
+defaultConfig :: BatchConfig
+defaultConfig = BatchConfig 0x5EED0001 0 1 2 2 0 1 0 1 0 0 256 0
+
+-- | BASELINE config 2: 2^20 instances, 1 proposer, 5 acceptors, no faults.
+config2 :: BatchConfig
+config2 = defaultConfig { bcSeed = 0x5EED0002, bcCount = 2 ^ (20 :: Int)
+                        , bcProposers = 1, bcAcceptors = 5 }
+
+data Flag = Undecided | Stuck | Panic | LogDivergence | StepCap
+          | QueueOverflow | TicketOverflow | LogTrunc
+  deriving (Show, Eq, Enum, Bounded)
+
+-- | One instance's outcome (pxb_result): the Proposal of the first Execute
+-- broadcast (Client.hs:178), the number of AskForTicket rounds, the steps the
+-- instance ran and its flags.
+data Outcome = Outcome
+  { oDecided :: Maybe Proposal
+  , oRounds  :: !Int
+  , oSteps   :: !Int
+  , oFlags   :: [Flag]
+  } deriving (Show)
+
+-- | Run totals (pxb_counters, slots of SURVEY.md §8(e)).
+data Totals = Totals
+  { tDecided, tUndecided, tStuck, tPanic, tDivergence, tStepCap
+  , tRounds, tMessages :: !Int64
+  } deriving (Show)
+
+-- | "c<clientId>.<t>" from the command code (Client.hs:202-203).
+commandOf :: Word32 -> Command
+commandOf code = "c" <> show (code `shiftR` 24) <> "." <> show (code .&. 0xFFFFFF)
+
+foreign import ccall safe "pxb_run"
+  c_pxb_run :: Ptr BatchConfig -> Ptr Word32 -> Ptr Word32 -> Ptr () -> Ptr Int64 -> IO CInt
+foreign import ccall safe "pxb_run_multi"
+  c_pxb_run_multi :: Ptr BatchConfig -> CInt -> Ptr Word32 -> Ptr Word32 -> Ptr () -> Ptr Int64 -> IO CInt
+foreign import ccall unsafe "pxb_strerror"
+  c_pxb_strerror :: CInt -> IO CString
+
+-- | Run a batch on the current GPU.
+runBatch :: BatchConfig -> IO (Either String ([Outcome], Totals))
+runBatch cfg = runWith cfg (\pc pres ptot -> c_pxb_run pc pres nullPtr nullPtr ptot)
+
+-- | Run a batch sharded over the first @g@ GPUs (all visible when @g <= 0@);
+-- totals are all-reduced with RCCL.  Outcomes are identical to 'runBatch'.
+runBatchMulti :: Int -> BatchConfig -> IO (Either String ([Outcome], Totals))
+runBatchMulti g cfg =
+  runWith cfg (\pc pres ptot -> c_pxb_run_multi pc (fromIntegral g) pres nullPtr nullPtr ptot)
+
+runWith :: BatchConfig
+        -> (Ptr BatchConfig -> Ptr Word32 -> Ptr Int64 -> IO CInt)
+        -> IO (Either String ([Outcome], Totals))
+runWith cfg call = do
+  let n = fromIntegral (bcCount cfg) :: Int
+  fres <- mallocForeignPtrArray (4 * n)          -- pinned: 16 B per instance
+  with cfg $ \pc ->
+    withForeignPtr fres $ \pres ->
+      allocaArray 16 $ \ptot -> do
+        rc <- call pc pres ptot
+        if rc /= 0
+          then Left <$> (c_pxb_strerror rc >>= peekCString)
+          else do
+            outs <- forM [0 .. n - 1] $ \i -> do
+              [v, t, r, f] <- peekArray 4 (advancePtr pres (4 * i))
+              pure (decode v t r f)
+            [d, u, s, p, dv, sc, rd, ms] <- peekArray 8 ptot
+            pure (Right (outs, Totals d u s p dv sc rd ms))
+
+decode :: Word32 -> Word32 -> Word32 -> Word32 -> Outcome
+decode v t r f = Outcome
+  { oDecided = if v == 0 then Nothing
+               else Just (Ticket (fromIntegral (fromIntegral t :: Int32)), commandOf v)
+  , oRounds  = fromIntegral r
+  , oSteps   = fromIntegral (f `shiftR` 16)
+  , oFlags   = [fl | fl <- [minBound .. maxBound], testBit f (fromEnum fl)]
+  }

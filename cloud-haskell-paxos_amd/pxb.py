@@ -166,6 +166,8 @@ def load(path: str = LIB_PATH):
     lib.pxb_run.restype = C.c_int
     lib.pxb_run_device.argtypes = [C.POINTER(pxb_config), vp, vp, vp, vp, vp]
     lib.pxb_run_device.restype = C.c_int
+    lib.pxb_run_multi.argtypes = [C.POINTER(pxb_config), C.c_int, vp, vp, vp, vp]
+    lib.pxb_run_multi.restype = C.c_int
     lib.pxb_acceptor_handle.argtypes = [vp, vp, vp, C.c_uint32]
     lib.pxb_acceptor_handle.restype = C.c_int
     lib.pxb_proposer_handle.argtypes = [vp, C.c_uint32, vp, vp, vp, C.c_uint32]
@@ -209,6 +211,22 @@ def run(cfg: Config, first_instance: int, n_instances: int, want_results=True,
     c = cfg.to_c(first_instance, n_instances)
     check(lib.pxb_run(C.byref(c), _ptr(res), _ptr(dig), _ptr(acc), C.cast(C.byref(tot), C.c_void_p)))
     return res, dig, acc, counters_dict(tot.c)
+
+
+def run_multi(cfg: Config, first_instance: int, n_instances: int, n_devices: int = 0,
+              want_results=True, want_digests=True):
+    """Host-buffer batch sharded over devices 0..n_devices-1 (pxb_run_multi):
+    one thread per GPU, one RCCL all-reduce of the run totals."""
+    import numpy as np
+    lib = load()
+    N = cfg.n_acceptors
+    res = np.zeros((n_instances, 4), dtype=np.uint32) if want_results else None
+    dig = np.zeros((n_instances, N), dtype=np.uint32) if want_digests else None
+    tot = pxb_counters()
+    c = cfg.to_c(first_instance, n_instances)
+    check(lib.pxb_run_multi(C.byref(c), n_devices, _ptr(res), _ptr(dig), None,
+                            C.cast(C.byref(tot), C.c_void_p)))
+    return res, dig, counters_dict(tot.c)
 
 
 def run_device(cfg: Config, first_instance: int, n_instances: int, d_results=None,

@@ -128,6 +128,14 @@ int pxb_run(const pxb_config* cfg, pxb_result* out, uint32_t* log_digest,
 int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_digest,
                    pxb_acceptor_rec* d_acc, int64_t* d_totals, void* stream);
 
+/* pxb_run_multi: HOST buffers, sharded over devices 0..n_devices-1 (<= 0: all
+ * visible) by contiguous global-instance ranges, one host thread per device;
+ * totals = one RCCL all-reduce (sum) of the per-device run totals over xGMI.
+ * Results are identical to pxb_run for any device count (Philox is keyed by
+ * the global instance id).  Replaces: Main.hs:37-53 for a multi-GPU node.     */
+int pxb_run_multi(const pxb_config* cfg, int n_devices, pxb_result* out, uint32_t* log_digest,
+                  pxb_acceptor_rec* acc, pxb_counters* totals);
+
 /* ---- single-handler hooks (run the kernel's own device functions) -------- */
 /* One message in or out.  Requests (ClientRequest, Common.hs:41-45):
  *   kind 0 AskForTicket t | 1 Propose (t, c) | 2 Execute t ; x = t, z = c.

@@ -184,3 +184,22 @@ def test_proposer_hook_matches_oracle(gpu_lib):
         gst = st.copy()
         gbc, gnb = pxb.proposer_handle(gst, N, msg)
         assert np.array_equal(gst, est) and np.array_equal(gbc, ebc) and np.array_equal(gnb, enb)
+
+
+def test_run_multi_matches_single_device(gpu_lib):
+    """pxb_run_multi (thread per GPU + RCCL all-reduce of the totals) on the
+    visible devices reproduces pxb_run bit-exact."""
+    cfg = pxb.CONFIGS[3]
+    res, dig, cnt = pxb.run_multi(cfg, 0, 20000)
+    eres, edig, _, ecnt = pxb.run(cfg, 0, 20000)
+    assert np.array_equal(res, eres) and np.array_equal(dig, edig) and cnt == ecnt
+
+
+def test_host_driver_binary(gpu_lib):
+    """The C++ batch driver (the app/Main.hs role) runs config 1 end to end."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(pxb.LIB_PATH), "..", "host", "paxos_batch_main")
+    out = subprocess.run([exe, "--config", "1", "--show", "2"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert "decided c1.1 @ Ticket 1, rounds 1, steps 6, flags -" in out.stdout
+    assert "decided          1024" in out.stdout
