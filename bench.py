@@ -29,6 +29,10 @@ import torch.distributed as dist  # noqa: E402
 import pxb  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+# HBM bytes per launch measured with rocprofv3 PMC passes (tools/profile_round.sh
+# + tools/traffic.py) for the default workload; rocprofv3 must wrap the process,
+# so bench.py reports the committed measurement of the same command.
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic_config2.json")
 
 
 def parse():
@@ -96,6 +100,19 @@ def run_workload(cfg, n, steps, warmup, rank, world, stream, dev):
     return float(elapsed.item()), kms, pxb.counters_dict(tot.cpu().tolist())
 
 
+def traffic_per_launch(c, n):
+    """PMC-measured HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE) from the
+    committed profile of this exact workload, else None."""
+    try:
+        with open(TRAFFIC_FILE) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if t.get("config") != c or t.get("instances") != n:
+        return None
+    return t.get("bytes_per_launch")
+
+
 def cpu_baseline(cfg, budget_s):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_c                          # CPU restatement (oracle/), baseline only
@@ -156,7 +173,7 @@ def main():
                    "randomize": cfg.randomize, "seed": hex(cfg.seed),
                    "parallelism": "instance-range shards x%d" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_per_launch(c, n),
                      "accounting": "SURVEY.md 8(d) canonical bytes (%.0f B/instance), "
                                    "kernel avg %.4f ms/launch (HIP events)" % (
                                        cnt["canon_bytes"] / max(1, cnt["instances"]), kms)},

@@ -22,8 +22,8 @@
 //   * waves are persistent: when a slot's instance quiesces (or hits
 //     step_cap) the slot writes its 16-B result + 4-B/acceptor digests and
 //     refills from the wave's contiguous instance range.
-//   * run totals are reduced from the result records by a second kernel, so
-//     the hot loop carries no counter state.
+//   * run totals: slot leaders count finished instances in packed 16-bit
+//     per-lane counters, reduced once per wave when the wave exits.
 //
 // Semantics: docs/SEMANTICS.md; checked bit-exact against oracle/.
 #include <hip/hip_runtime.h>
@@ -74,7 +74,7 @@ struct KParams {
   uint32_t loss_m1, crash_m1;         // thr-1 (valid when LOSSY / CRASHY)
   uint32_t loss_ppm, crash_ppm;       // maxima for RANDOMIZE
   uint32_t crash_len_max, crash_start_max, skew_max, step_cap;
-  uint4* out;                         // pxb_result records (never null)
+  uint4* out;                         // pxb_result records (nullable)
   uint32_t* dig;
   uint4* acc;
   unsigned long long* totals;
@@ -205,6 +205,11 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
   Link R[PM], Sx[PM];                     // lane: links p -> a, a -> p
   uint32_t msgs_acc = 0;                  // lane totals across instances
   uint64_t canon_acc = 0;
+  // slot-leader run totals, two 16-bit counts per register (the host sizes
+  // launches so no slot finishes 65536 instances):
+  //   ca = instances | undecided<<16, cb = stuck | panic<<16,
+  //   cc = divergence | step_cap<<16, cd = queue_ovf | ticket_ovf<<16, ce = log_trunc
+  uint32_t ca = 0, cb = 0, cc = 0, cd = 0, ce = 0, rounds_acc = 0, steps_acc = 0;
 #pragma unroll
   for (int p = 0; p < PM; ++p) {
     S[p] = PropState{0, 0, 0, IDLE, 0, 0, 0, 0, false};
@@ -566,6 +571,15 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
           f |= (!cap && (uint32_t)p < P && S[p].rs != IDLE) ? (uint32_t)PXB_F_STUCK : 0u;
         canon_acc += (a == 0) ? 20u : 4u;          // result record + this digest
         if (a == 0) {
+          ca += 1u + ((f & PXB_F_UNDECIDED) ? 0x10000u : 0u);
+          cb += ((f & PXB_F_STUCK) ? 1u : 0u) + ((f & PXB_F_PANIC) ? 0x10000u : 0u);
+          cc += ((f & PXB_F_LOG_DIVERGENCE) ? 1u : 0u) + ((f & PXB_F_STEP_CAP) ? 0x10000u : 0u);
+          cd += ((f & PXB_F_QUEUE_OVERFLOW) ? 1u : 0u) + ((f & PXB_F_TICKET_OVERFLOW) ? 0x10000u : 0u);
+          ce += (f & PXB_F_LOG_TRUNC) ? 1u : 0u;
+          rounds_acc += rounds;
+          steps_acc += (uint32_t)s;
+        }
+        if (a == 0 && kp.out) {
           uint4 r;
           r.x = dval ? ((dval << 24) | 1u) : 0u;
           r.y = dval ? (uint32_t)dtick : 0u;
@@ -590,73 +604,30 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
 
   STAMP(6);
   STAMP_FLUSH(kp.dbg);
-  // ---------------- flush lane totals (messages, canonical bytes) ------------
-  uint32_t m = msgs_acc;
+  // ---------------- flush lane totals -----------------------------------------
+  uint32_t v[13] = {ca & 0xFFFFu, ca >> 16, cb & 0xFFFFu, cb >> 16, cc & 0xFFFFu, cc >> 16,
+                    cd & 0xFFFFu, cd >> 16, ce, rounds_acc, steps_acc, msgs_acc, 0u};
   uint64_t c64 = canon_acc;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
-    m += (uint32_t)__shfl_xor((int)m, off);
+#pragma unroll
+    for (int q = 0; q < 12; ++q) v[q] += (uint32_t)__shfl_xor((int)v[q], off);
     const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)c64, off);
     const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(c64 >> 32), off);
     c64 += ((uint64_t)hi << 32) | lo;
   }
-  if (lane == 0) {
-    atomicAdd(&kp.totals[PXB_C_MESSAGES], (unsigned long long)m);
-    atomicAdd(&kp.totals[PXB_C_CANON_BYTES], (unsigned long long)c64);
-  }
-}
-
-// ---- run totals from the result records ---------------------------------------
-// (decided / undecided / flag counts / rounds / steps / instances)
-constexpr int RED_BLOCK = 256;
-__global__ __launch_bounds__(RED_BLOCK) void reduce_results_kernel(const uint4* __restrict__ res, uint32_t n,
-                                                                   unsigned long long* totals) {
-  // per-thread partial counts: [0] instances [1] undecided [2] stuck [3] panic
-  // [4] divergence [5] step_cap [6] rounds [7] steps [8] qovf [9] tovf [10] trunc
-  uint32_t c[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  for (uint32_t i = blockIdx.x * RED_BLOCK + threadIdx.x; i < n; i += gridDim.x * RED_BLOCK) {
-    const uint4 r = res[i];
-    const uint32_t f = r.w;
-    c[0] += 1u;
-    c[1] += f & 1u;
-    c[2] += (f >> 1) & 1u;
-    c[3] += (f >> 2) & 1u;
-    c[4] += (f >> 3) & 1u;
-    c[5] += (f >> 4) & 1u;
-    c[8] += (f >> 5) & 1u;
-    c[9] += (f >> 6) & 1u;
-    c[10] += (f >> 7) & 1u;
-    c[6] += r.z;
-    c[7] += f >> 16;
-  }
-  __shared__ uint32_t part[RED_BLOCK / 64][11];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane < 13) {
+    // lane q adds counter q (one atomic per lane, no serialisation within the wave)
+    const int slot_of[13] = {PXB_C_INSTANCES, PXB_C_UNDECIDED, PXB_C_STUCK, PXB_C_PANIC, PXB_C_DIVERGENCE,
+                             PXB_C_STEP_CAP, PXB_C_QUEUE_OVERFLOW, PXB_C_TICKET_OVERFLOW, PXB_C_LOG_TRUNC,
+                             PXB_C_ROUNDS, PXB_C_STEPS, PXB_C_MESSAGES, PXB_C_DECIDED};
+    unsigned long long val = 0;
 #pragma unroll
-  for (int k = 0; k < 11; ++k) {
-    uint32_t v = c[k];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += (uint32_t)__shfl_xor((int)v, off);
-    if (lane == 0) part[w][k] = v;
+    for (int q = 0; q < 12; ++q) val = (lane == q) ? (unsigned long long)v[q] : val;
+    if (lane == 12) val = (unsigned long long)v[0] - (unsigned long long)v[1];   // decided
+    if (val) atomicAdd(&kp.totals[slot_of[lane]], val);
   }
-  __syncthreads();
-  if (threadIdx.x < 11) {
-    unsigned long long v = 0;
-#pragma unroll
-    for (int q = 0; q < RED_BLOCK / 64; ++q) v += part[q][threadIdx.x];
-    const int slot[11] = {PXB_C_INSTANCES, PXB_C_UNDECIDED, PXB_C_STUCK, PXB_C_PANIC,
-                          PXB_C_DIVERGENCE, PXB_C_STEP_CAP, PXB_C_ROUNDS, PXB_C_STEPS,
-                          PXB_C_QUEUE_OVERFLOW, PXB_C_TICKET_OVERFLOW, PXB_C_LOG_TRUNC};
-    if (v) atomicAdd(&totals[slot[threadIdx.x]], v);
-  }
-  if (threadIdx.x == 0) {
-    unsigned long long inst = 0, und = 0;
-#pragma unroll
-    for (int q = 0; q < RED_BLOCK / 64; ++q) {
-      inst += part[q][0];
-      und += part[q][1];
-    }
-    if (inst - und) atomicAdd(&totals[PXB_C_DECIDED], inst - und);
-  }
+  if (lane == 13) atomicAdd(&kp.totals[PXB_C_CANON_BYTES], (unsigned long long)c64);
 }
 
 // ---- single-handler hook kernels ------------------------------------------
@@ -733,8 +704,6 @@ static unsigned long long* g_dbg = nullptr;
 static std::mutex g_mu;
 static int g_occ[4][10][64];            // [pm][n][device] blocks per CU (0 = unknown)
 static int g_cus[64];
-static void* g_scratch[64];             // per device: result records when the caller passes none
-static size_t g_scratch_bytes[64];
 
 static int hip_fail(hipError_t e) {
   g_last_hip = (int)e;
@@ -805,11 +774,7 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
   kernel_fn fn = pick(cfg->n_proposers, cfg->n_acceptors);
   if (!fn) return PXB_E_INVAL;
   const hipStream_t st = (hipStream_t)stream;
-  // without caller-provided result records the run goes through a cached
-  // scratch buffer in chunks (the totals are reduced from those records)
-  const uint64_t chunk_max = d_out ? (1ull << 31) : (1ull << 24);
   int occ, cus;
-  uint4* scratch = nullptr;
   {
     std::lock_guard<std::mutex> lk(g_mu);
     if (!g_cus[dev]) {
@@ -827,17 +792,6 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
     cus = g_cus[dev];
     static const char* cap_env = getenv("PXB_BLOCKS_PER_CU");   // experiments: cap residency
     if (cap_env && atoi(cap_env) > 0) occ = std::min(occ, atoi(cap_env));
-    if (!d_out) {
-      const size_t need = (size_t)std::min<uint64_t>(cfg->n_instances, chunk_max) * sizeof(uint4);
-      if (g_scratch_bytes[dev] < need) {
-        if (g_scratch[dev]) (void)hipFree(g_scratch[dev]);
-        g_scratch[dev] = nullptr;
-        g_scratch_bytes[dev] = 0;
-        HIPCHK(hipMalloc(&g_scratch[dev], need));
-        g_scratch_bytes[dev] = need;
-      }
-      scratch = (uint4*)g_scratch[dev];
-    }
   }
   KParams kp;
   memset(&kp, 0, sizeof(kp));
@@ -869,20 +823,19 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
 #endif
   const uint64_t G = 64 / cfg->n_acceptors;
   const uint64_t resident = (uint64_t)occ * (uint64_t)cus;
+  // a launch must not give any slot 65536 instances (16-bit packed run totals)
+  const uint64_t chunk_max = std::min<uint64_t>(1ull << 31, resident * WPB * G * 60000ull);
   for (uint64_t done = 0; done < cfg->n_instances; done += chunk_max) {
     const uint64_t nc = std::min<uint64_t>(chunk_max, cfg->n_instances - done);
     kp.first_instance = cfg->first_instance + done;
     kp.n_instances = (uint32_t)nc;
-    kp.out = d_out ? reinterpret_cast<uint4*>(d_out + done) : scratch;
+    kp.out = d_out ? reinterpret_cast<uint4*>(d_out + done) : nullptr;
     kp.dig = d_log_digest ? d_log_digest + done * cfg->n_acceptors : nullptr;
     kp.acc = d_acc ? reinterpret_cast<uint4*>(d_acc + done * cfg->n_acceptors) : nullptr;
     const uint64_t waves_needed = (nc + G - 1) / G;
     const uint64_t blocks_needed = (waves_needed + WPB - 1) / WPB;
     const unsigned grid = (unsigned)std::min<uint64_t>(blocks_needed, resident);
     hipLaunchKernelGGL(fn, dim3(grid), dim3(BLOCK), 0, st, kp);
-    HIPCHK(hipGetLastError());
-    const unsigned rgrid = (unsigned)std::min<uint64_t>((nc + RED_BLOCK - 1) / RED_BLOCK, (uint64_t)cus * 4);
-    hipLaunchKernelGGL(reduce_results_kernel, dim3(rgrid), dim3(RED_BLOCK), 0, st, kp.out, (uint32_t)nc, kp.totals);
     HIPCHK(hipGetLastError());
   }
   return PXB_OK;
