@@ -128,22 +128,23 @@ __device__ __forceinline__ void static_for(F&& f) {
 // nibble shift-queue, so "how many are due now" needs no LDS access.
 struct Link {
   uint32_t dn;    // due&15 of entry i in bits [4i+3:4i], entry 0 = head
-  uint32_t hl;    // head[2:0] | len[6:3] | last_due[31:8]
+  uint32_t hl;    // len[3:0] | head[6:4] | 0[7] | last_due[31:8]
   uint32_t seq;   // sends attempted on this link (Philox counter word 2)
 };
-__device__ __forceinline__ uint32_t l_len(const Link& L) { return (L.hl >> 3) & 15u; }
-__device__ __forceinline__ uint32_t l_head(const Link& L) { return L.hl & 7u; }
+__device__ __forceinline__ uint32_t l_len(const Link& L) { return L.hl & 15u; }
+__device__ __forceinline__ uint32_t l_head(const Link& L) { return (L.hl >> 4) & 7u; }
 __device__ __forceinline__ int32_t l_last(const Link& L) { return (int32_t)(L.hl >> 8); }
-// number of entries at the head that are due at step s (due == s <=> nibble == s&15,
-// because every queued due lies in [s, s+15])
-__device__ __forceinline__ uint32_t l_due_count(const Link& L, uint32_t s4) {
-  const uint32_t x = L.dn ^ (s4 * 0x11111111u);
-  const uint32_t tz = x ? (uint32_t)__builtin_ctz(x) : 32u;
-  return min(tz >> 2, l_len(L));
+// find-first-set-bit with the hardware's "none" value (v_ffbl_b32: ~0u for 0)
+__device__ __forceinline__ uint32_t ffbl(uint32_t x) { return x ? (uint32_t)__builtin_ctz(x) : ~0u; }
+// number of entries at the head that are due at step s (due == s <=> nibble ==
+// s&15, because every queued due lies in [s, s+15]); srep = (s&15) * 0x11111111
+__device__ __forceinline__ uint32_t l_due_count(const Link& L, uint32_t srep) {
+  return min(ffbl(L.dn ^ srep) >> 2, l_len(L));
 }
-__device__ __forceinline__ void l_pop(Link& L) {
-  L.dn >>= 4;
-  L.hl = (L.hl & ~0x7Fu) | ((L.hl + 1u) & 7u) | ((l_len(L) - 1u) << 3);
+// pop the head when `p`: len - 1, head + 1 (mod 8: the carry into bit 7 is cleared)
+__device__ __forceinline__ void l_pop_if(Link& L, bool p) {
+  L.dn = p ? (L.dn >> 4) : L.dn;
+  L.hl = p ? ((L.hl + 15u) & ~0x80u) : L.hl;
 }
 
 template <int PM, int N>
@@ -164,6 +165,7 @@ template <int PM, int N>
 __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KParams kp) {
   constexpr int G = 64 / N;
   constexpr uint32_t NM = (1u << N) - 1u;     // slot-local lane mask
+  constexpr uint32_t ENONE = 16u;             // "no event" acceptor index (N <= 9 < 16)
   __shared__ Lds<PM, N> s_lds[WPB];
 
   const int lane = threadIdx.x & 63;
@@ -200,6 +202,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
   int32_t c0 = 0, c1 = 0;                 // lane: isolation window of acceptor a
   AccState A{0, 0, 0, false};             // lane: acceptor a (ServerState)
   uint32_t log_len = 0, lflags = 0, digest = 0;   // lane
+  uint32_t canon = 0;                     // lane: canonical bytes of the current instance
   PropState S[PM];                        // replicated proposers (ClientState)
   int32_t skew[PM];
   Link R[PM], Sx[PM];                     // lane: links p -> a, a -> p
@@ -218,14 +221,15 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
     Sx[p] = Link{0, 0, 0};
   }
 
-  // common link send (docs/SEMANTICS.md §5): Philox loss/delay, FIFO due,
-  // bounded ring (overflow -> flag, message dropped)
-  auto link_send = [&](Link& Lk, uint32_t* ring, uint32_t dirbits, uint32_t word) {
-    msgs_acc++;
-    const uint32_t k = Lk.seq++;
+  // common link send, predicated on `pred` (docs/SEMANTICS.md §5): Philox
+  // loss/delay, FIFO due, bounded ring (overflow -> flag, message dropped)
+  auto link_send = [&](Link& Lk, uint32_t* ring, uint32_t dirbits, uint32_t word, bool pred) {
+    msgs_acc += pred ? 1u : 0u;
+    const uint32_t k = Lk.seq;
+    Lk.seq = pred ? k + 1u : k;
     int32_t d = 1;
     bool ok = true;
-    if (faulty) {
+    if (pred && faulty) {
       const uint64_t inst = kp.first_instance + idx;
       const uint4 w = philox((uint32_t)inst, (uint32_t)(inst >> 32), k, (1u << 24) | dirbits | (uint32_t)a, k0, k1);
       ok = !(lossy && w.x <= loss_m1);
@@ -233,23 +237,55 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
     }
     const uint32_t len = l_len(Lk);
     const bool full = len >= (uint32_t)QD;
-    const bool push = ok && !full;
-    lflags |= (ok && full) ? (uint32_t)PXB_F_QUEUE_OVERFLOW : 0u;
+    const bool push = pred && ok && !full;
+    const bool ovf = pred && ok && full;
+    if (any(ovf)) lflags |= ovf ? (uint32_t)PXB_F_QUEUE_OVERFLOW : 0u;
     const int32_t due = max(s + d, l_last(Lk));
     if (push) ring[((l_head(Lk) + len) & 7u) * 64u + (uint32_t)lane] = word;
     Lk.dn = push ? (Lk.dn | (((uint32_t)due & 15u) << (4u * len))) : Lk.dn;
-    Lk.hl = push ? ((Lk.hl & 7u) | ((len + 1u) << 3) | ((uint32_t)due << 8)) : Lk.hl;
+    Lk.hl = push ? (((Lk.hl & 0x7Fu) + 1u) | ((uint32_t)due << 8)) : Lk.hl;
   };
   // proposer p's broadcast copy on link p -> a (sendToAllServers, Client.hs:122-123)
   auto send_req = [&](auto pc, bool has, uint32_t kind, int32_t x, uint32_t z) {
     constexpr int p = decltype(pc)::value;
-    if (!has) return;
-    rounds += (kind == ASK) ? 1u : 0u;
-    if (kind == EXECUTE && dval == 0u) {   // first Execute: the decided value
-      dval = S[p].r2_v;
-      dtick = x;
+    rounds += (has && kind == ASK) ? 1u : 0u;
+    const bool first_exec = has && kind == EXECUTE && dval == 0u;   // the decided value
+    dval = first_exec ? S[p].r2_v : dval;
+    dtick = first_exec ? x : dtick;
+    link_send(R[p], &L.rq[p][0][0], (uint32_t)p << 8, (uint32_t)x | (z << 14) | (kind << 16), has);
+  };
+  // one request from the head of link p -> a, predicated on `due`:
+  // handleClientRequest, Server.hs:51-78 (dead / isolated acceptors discard it)
+  auto acc_take = [&](auto pc, bool due, bool isolated) {
+    constexpr int p = decltype(pc)::value;
+    const uint32_t w = L.rq[p][l_head(R[p])][lane];
+    l_pop_if(R[p], due);
+    const uint32_t kind = (w >> 16) & 3u;
+    const bool live = due && !A.dead && !isolated;
+    const uint32_t rb = 8u + ((kind & 1u) << 2);       // payload: Propose 12, Ask / Execute 8
+    canon += live ? 2u * rb + 32u : (due ? rb : 0u);    // discarded: written, not read
+    int32_t rx, ry;
+    uint32_t rz, ev;
+    const uint32_t rk = acceptor_step(A, live, kind, (int32_t)(w & 0x3FFFu), (w >> 14) & 3u, rx, ry, rz, ev);
+    if (any(ev != 0u)) {
+      if (ev != 0u) {
+        digest = fnv_u32(digest, (ev << 24) | 1u);
+        if (log_len < (uint32_t)LT) {
+          // two acceptors of this instance executed different commands at
+          // the same position iff the max already holds this epoch with
+          // another command (order-independent, SEMANTICS §7)
+          const uint32_t tag = idx - first_idx + 1u;
+          const uint32_t old = atomicMax(&clog[log_len], (tag << 2) | ev);
+          if ((old >> 2) == tag && (old & 3u) != ev) lflags |= PXB_F_LOG_DIVERGENCE;
+        } else {
+          lflags |= PXB_F_LOG_TRUNC;
+        }
+        log_len++;
+      }
     }
-    link_send(R[p], &L.rq[p][0][0], (uint32_t)p << 8, ((uint32_t)x & 0x3FFFu) | (z << 14) | (kind << 16));
+    // tickets are < 2^14 (SEMANTICS §6), so the fields need no masking
+    link_send(Sx[p], &L.sq[p][0][0], (1u << 16) | ((uint32_t)p << 8),
+              (uint32_t)rx | ((uint32_t)ry << 14) | (rz << 28) | (rk << 30), rk != NONE);
   };
 
   STAMP_DECL
@@ -303,6 +339,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
         tovf = false;
         A = AccState{0, 0, 0, false};
         log_len = lflags = 0;
+        canon = 0;
         digest = 0x811C9DC5u;
         rounds = dval = 0;
         dtick = 0;
@@ -314,48 +351,21 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
     if (!any(active)) break;
     STAMP(0);
 
-    const uint32_t s4 = (uint32_t)s & 15u;
+    const uint32_t srep = ((uint32_t)s & 15u) * 0x11111111u;
     // ---------------- acceptor phase: (proposer index, link seq) order -------
-    // handleClientRequest, Server.hs:51-78, for every due request of lane a
+    // handleClientRequest, Server.hs:51-78, for every due request of lane a;
+    // the first due request of every lane is handled straight-line, further
+    // ones (delay > 1 bunching) in a loop.
     {
       const bool isolated = (c0 <= s) && (s < c1);
       static_for<0, PM>([&](auto pc) {
         constexpr int p = decltype(pc)::value;
-        for (;;) {
-          const bool due = active && l_len(R[p]) > 0u && (R[p].dn & 15u) == s4;
-          if (!any(due)) break;
-          if (due) {
-            const uint32_t w = L.rq[p][l_head(R[p])][lane];
-            l_pop(R[p]);
-            const uint32_t kind = (w >> 16) & 3u;
-            const uint32_t rb = (kind == PROPOSE) ? 12u : 8u;
-            const bool live = !A.dead && !isolated;
-            canon_acc += live ? 2u * rb + 32u : rb;        // discarded: written, not read
-            if (live) {
-              int32_t rx, ry;
-              uint32_t rz, ev;
-              const uint32_t rk = acceptor_step(A, kind, (int32_t)(w & 0x3FFFu), (w >> 14) & 3u,
-                                                rx, ry, rz, ev);
-              lflags |= A.dead ? (uint32_t)PXB_F_PANIC : 0u;
-              if (ev != 0u) {
-                digest = fnv_u32(digest, (ev << 24) | 1u);
-                if (log_len < (uint32_t)LT) {
-                  // two acceptors of this instance executed different commands at
-                  // the same position iff the max already holds this epoch with
-                  // another command (order-independent, SEMANTICS §7)
-                  const uint32_t tag = idx - first_idx + 1u;
-                  const uint32_t old = atomicMax(&clog[log_len], (tag << 2) | ev);
-                  if ((old >> 2) == tag && (old & 3u) != ev) lflags |= PXB_F_LOG_DIVERGENCE;
-                } else {
-                  lflags |= PXB_F_LOG_TRUNC;
-                }
-                log_len++;
-              }
-              if (rk != NONE)
-                link_send(Sx[p], &L.sq[p][0][0], (1u << 16) | ((uint32_t)p << 8),
-                          ((uint32_t)rx & 0x3FFFu) | (((uint32_t)ry & 0x3FFFu) << 14) | (rz << 28) | (rk << 30));
-            }
-          }
+        uint32_t cnt = active ? l_due_count(R[p], srep) : 0u;
+        if (any(cnt > 0u)) {
+          do {
+            acc_take(pc, cnt > 0u, isolated);
+            cnt = (cnt > 0u) ? cnt - 1u : 0u;
+          } while (any(cnt > 0u));
         }
       });
     }
@@ -376,7 +386,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
         }
         send_req(pc, no > 0u, o0.kind, o0.x, o0.z);
       }
-      const uint32_t cnt_p = pact ? l_due_count(Sx[p], s4) : 0u;
+      const uint32_t cnt_p = pact ? l_due_count(Sx[p], srep) : 0u;
       const uint64_t anyb = ballot(cnt_p > 0u);
       STAMP(2);
       if (anyb != 0ull) {
@@ -391,19 +401,22 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
         // slot max-reduction of (t_store, -lane) over the counted acks.  After
         // an event only a NACK (not Idle) or a stale Round2Success (in Round2)
         // can still act: a fresh Round1OK for the new ticket cannot exist yet.
+        // Every round is a select network (no divergent branches).
         const bool fast = pact && !slot_serial && mine_slot != 0u;
         if (any(fast)) {
           const bool has = fast && cnt_p == 1u;
-          const uint32_t w = has ? L.sq[p][l_head(Sx[p])][lane] : 0u;
-          const uint32_t kind = w >> 30;
+          const uint32_t w = L.sq[p][l_head(Sx[p])][lane];
+          l_pop_if(Sx[p], has);
+          const uint32_t kind = has ? (w >> 30) : 3u;       // 3: no response
           const int32_t x = (int32_t)(w & 0x3FFFu);
           const int32_t y = (int32_t)((w >> 14) & 0x3FFFu);
-          const uint32_t z = (w >> 28) & 3u;
+          const uint32_t z = has ? ((w >> 28) & 3u) : 0u;
+          canon += has ? 2u * (16u >> kind) : 0u;
           uint32_t rem = slot(ballot(has));                 // unprocessed responses
-          const uint32_t havem = slot(ballot(has && kind == HAVE));
-          const uint32_t r2sm = slot(ballot(has && kind == R2S));
+          const uint32_t havem = slot(ballot(kind == HAVE));
+          const uint32_t r2sm = slot(ballot(kind == R2S));
           bool go = fast;
-          while (any(go)) {
+          do {
             PropState& Sp = S[p];
             const uint32_t rs = Sp.rs;
             const int32_t T = Sp.ticket;
@@ -416,11 +429,12 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
             const uint32_t need = (uint32_t)(N >> 1) + 1u - Sp.acks;
             const bool is_maj = is_ack && (uint32_t)__popc(ackm & ltm) + 1u == need;
             const uint32_t majm = slot(ballot(is_maj));
-            const uint32_t e_ab = abm ? (uint32_t)__builtin_ctz(abm) : 32u;
-            const uint32_t e_mj = majm ? (uint32_t)__builtin_ctz(majm) : 32u;
+            const uint32_t e_ab = min(ffbl(abm), ENONE);
+            const uint32_t e_mj = min(ffbl(majm), ENONE);
+            const bool mj = e_mj < e_ab;                    // majority before any NACK
             const uint32_t e = min(e_ab, e_mj);
-            const uint32_t below_e = (e >= 32u) ? ~0u : ((1u << e) - 1u);
-            const uint32_t counted = (ackm & below_e) | ((e_mj < e_ab) ? (1u << e_mj) : 0u);
+            // acks counted before the event (and the majority ack itself)
+            const uint32_t counted = ackm & ((1u << (e + (mj ? 1u : 0u))) - 1u);
             // MostRecent over the counted Round1OKs that carry a proposal
             const bool elig = rs == ROUND1 && ((counted >> a) & 1u) != 0u && z != 0u;
             const uint32_t zb = slot(ballot(elig));
@@ -438,72 +452,40 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
               key = (uint32_t)__shfl((int)key, src);
               bz = (uint32_t)__shfl((int)z, zb ? base + 31 - (int)(key & 31u) : lane);
             }
-            uint32_t u = 0;
-            if (any(abm != 0u)) u = (uint32_t)__shfl(x, e_ab < 32u ? base + (int)e_ab : lane);
-            Req o0{NONE, 0, 0}, o1{NONE, 0, 0};
-            uint32_t no = 0;
-            if (go) {
-              int32_t mt = Sp.mr_t;
-              uint32_t mv = Sp.mr_v;
-              if (zb != 0u && (mv == 0u || (int32_t)(key >> 5) > mt)) {
-                mt = (int32_t)(key >> 5);
-                mv = bz;
-              }
-              Sp.acks += (uint32_t)__popc(counted);
-              if (e >= 32u) {                      // no event: only acks
-                if (rs == ROUND1) {
-                  Sp.mr_t = mt;
-                  Sp.mr_v = mv;
-                }
-              } else if (e_mj < e_ab) {            // majority reached at acceptor e
-                if (rs == ROUND1) {                // Client.hs:157-170
-                  Sp.r2_v = (mv == 0u) ? Sp.cmd : mv;
-                  Sp.pending = (mv != 0u);
-                  Sp.acks = 0;
-                  Sp.rs = ROUND2;
-                  Sp.mr_t = 0;
-                  Sp.mr_v = 0;
-                  o0 = Req{PROPOSE, T, Sp.r2_v};
-                  no = 1;
-                } else {                           // Client.hs:177-189
-                  o0 = Req{EXECUTE, T, 0};
-                  if (Sp.pending) {
-                    Sp.ticket = T + 1;
-                    Sp.acks = 0;
-                    Sp.rs = ROUND1;
-                    Sp.mr_t = 0;
-                    Sp.mr_v = 0;
-                    o1 = Req{ASK, T + 1, 0};
-                    no = 2;
-                  } else {
-                    Sp.cmd = 0;
-                    Sp.acks = 0;
-                    Sp.rs = IDLE;
-                    no = 1;
-                  }
-                }
-              } else {                             // HaveTicket u >= ticket, Client.hs:130-140
-                Sp.ticket = (int32_t)u + 1;
-                Sp.acks = 0;
-                Sp.rs = ROUND1;
-                Sp.mr_t = 0;
-                Sp.mr_v = 0;
-                o0 = Req{ASK, (int32_t)u + 1, 0};
-                no = 1;
-              }
-              rem &= (e >= 32u) ? 0u : ~(below_e | (1u << e));
-              go = Sp.rs != IDLE && (rem & (havem | (Sp.rs == ROUND2 ? r2sm : 0u))) != 0u;
-            }
-#pragma unroll 1
-            for (uint32_t k = 0; k < 2u; ++k) {
-              const bool hs = no > k;
-              if (any(hs)) send_req(pc, hs, k ? o1.kind : o0.kind, k ? o1.x : o0.x, k ? o1.z : o0.z);
-            }
-          }
-          if (has) {
-            canon_acc += 2u * (16u >> kind);
-            l_pop(Sx[p]);
-          }
+            int32_t u = 0;
+            if (any(abm != 0u)) u = __shfl(x, abm ? base + (int)e_ab : lane);
+            // ---- the state transition of this round (Client.hs:128-189) ----
+            int32_t mt = Sp.mr_t;
+            uint32_t mv = Sp.mr_v;
+            const bool take = zb != 0u && (mv == 0u || (int32_t)(key >> 5) > mt);
+            mt = take ? (int32_t)(key >> 5) : mt;
+            mv = take ? bz : mv;
+            const bool ev = go && e != ENONE;
+            const bool r1maj = go && mj && rs == ROUND1;    // Client.hs:157-170
+            const bool r2maj = go && mj && rs == ROUND2;    // Client.hs:177-189
+            const bool nack = ev && !mj;                    // Client.hs:130-140
+            const bool restart = r2maj && Sp.pending;       // Client.hs:179-185
+            const bool idle = r2maj && !Sp.pending;         // Client.hs:186-189
+            const uint32_t r2v = (mv == 0u) ? Sp.cmd : mv;
+            const int32_t tn = nack ? u + 1 : T + 1;
+            // outputs: o0 (Propose / Execute / AskForTicket), o1 (AskForTicket on restart)
+            const uint32_t k0o = r1maj ? PROPOSE : (r2maj ? EXECUTE : ASK);
+            const int32_t x0o = nack ? tn : T;
+            const uint32_t z0o = r1maj ? r2v : 0u;
+            Sp.r2_v = r1maj ? r2v : Sp.r2_v;
+            Sp.pending = r1maj ? (mv != 0u) : Sp.pending;
+            Sp.ticket = (nack || restart) ? tn : T;
+            Sp.cmd = idle ? 0u : Sp.cmd;
+            Sp.acks = go ? (ev ? 0u : Sp.acks + (uint32_t)__popc(counted)) : Sp.acks;
+            Sp.rs = r1maj ? ROUND2 : ((nack || restart) ? ROUND1 : (idle ? IDLE : rs));
+            const bool keep_mr = go && !ev && rs == ROUND1;
+            Sp.mr_t = keep_mr ? mt : (ev ? 0 : Sp.mr_t);
+            Sp.mr_v = keep_mr ? mv : (ev ? 0u : Sp.mr_v);
+            rem = ev ? rem & ~((2u << e) - 1u) : 0u;
+            go = ev && Sp.rs != IDLE && (rem & (havem | (Sp.rs == ROUND2 ? r2sm : 0u))) != 0u;
+            if (any(ev)) send_req(pc, ev, k0o, x0o, z0o);
+            if (any(restart)) send_req(pc, restart, ASK, tn, 0u);
+          } while (any(go));
         }
         STAMP(3);
         // ---- general path (a link holds >= 2 due responses): serial fold in
@@ -513,9 +495,9 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
         if (any(cnt_s > 0u)) {
 #pragma unroll 1
           for (int aa = 0; aa < N; ++aa) {
-            uint32_t ca = (uint32_t)__shfl((int)cnt_s, base + aa);
-            while (any(ca > 0u)) {
-              const bool take = ca > 0u;
+            uint32_t ca_ = (uint32_t)__shfl((int)cnt_s, base + aa);
+            while (any(ca_ > 0u)) {
+              const bool take = ca_ > 0u;
               const uint32_t mine = L.sq[p][l_head(Sx[p])][lane];
               const uint32_t w = (uint32_t)__shfl((int)mine, base + aa);
               Req o0{NONE, 0, 0}, o1{NONE, 0, 0};
@@ -524,11 +506,9 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
                 const uint32_t kind = w >> 30;
                 no = proposer_step(S[p], (uint32_t)N, kind, (int32_t)(w & 0x3FFFu),
                                    (int32_t)((w >> 14) & 0x3FFFu), (w >> 28) & 3u, o0, o1);
-                if (a == aa) {
-                  canon_acc += 2u * (16u >> kind);
-                  l_pop(Sx[p]);
-                }
-                ca--;
+                if (a == aa) canon += 2u * (16u >> kind);
+                l_pop_if(Sx[p], a == aa);
+                ca_--;
               }
 #pragma unroll 1
               for (uint32_t k = 0; k < 2u; ++k) {
@@ -539,7 +519,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
           }
         }
       }
-      canon_acc += (stepped && a == 0) ? 48u : 0u;
+      canon += (stepped && a == 0) ? 48u : 0u;
       tovf = tovf || (pact && S[p].ticket >= PXB_TICKET_LIMIT);
     });
     STAMP(4);
@@ -548,13 +528,13 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
     uint32_t lens = 0;
 #pragma unroll
     for (int p = 0; p < PM; ++p) lens |= R[p].hl | Sx[p].hl;
-    const uint64_t busyb = ballot(active && (lens & 0x78u) != 0u);
+    const uint64_t busyb = ballot(active && (lens & 15u) != 0u);
     const bool quiet = active && slot(busyb) == 0u && s >= last_tick;
     const bool cap = active && !quiet && (s + 1 >= (int32_t)kp.step_cap);
     s += active ? 1 : 0;
     const bool done = quiet || cap;
     if (any(done)) {
-      const uint32_t pan = slot(ballot((lflags & PXB_F_PANIC) != 0u));
+      const uint32_t pan = slot(ballot(A.dead));             // Q6: dead <=> panicked
       const uint32_t dvg = slot(ballot((lflags & PXB_F_LOG_DIVERGENCE) != 0u));
       const uint32_t qov = slot(ballot((lflags & PXB_F_QUEUE_OVERFLOW) != 0u));
       const uint32_t trc = slot(ballot((lflags & PXB_F_LOG_TRUNC) != 0u));
@@ -569,7 +549,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
 #pragma unroll
         for (int p = 0; p < PM; ++p)
           f |= (!cap && (uint32_t)p < P && S[p].rs != IDLE) ? (uint32_t)PXB_F_STUCK : 0u;
-        canon_acc += (a == 0) ? 20u : 4u;          // result record + this digest
+        canon_acc += canon + ((a == 0) ? 20u : 4u);          // + result record + this digest
         if (a == 0) {
           ca += 1u + ((f & PXB_F_UNDECIDED) ? 0x10000u : 0u);
           cb += ((f & PXB_F_STUCK) ? 1u : 0u) + ((f & PXB_F_PANIC) ? 0x10000u : 0u);
@@ -640,7 +620,7 @@ __global__ void acceptor_hook_kernel(pxb_acceptor_rec* st, const pxb_msg* in, px
   if (!A.dead) {
     int32_t rx, ry;
     uint32_t rz, ev;
-    const uint32_t rk = acceptor_step(A, in[i].kind, in[i].x, in[i].z, rx, ry, rz, ev);
+    const uint32_t rk = acceptor_step(A, true, in[i].kind, in[i].x, in[i].z, rx, ry, rz, ev);
     if (ev) log_len++;
     if (rk != NONE) r = pxb_msg{rk, rx, ry, rz};
   }

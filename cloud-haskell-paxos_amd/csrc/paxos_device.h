@@ -62,18 +62,20 @@ struct AccState {
 // Returns the reply tag (or NONE).  exec_val != 0 when `executed <>= [c]` ran.
 // Written as selects (no branches): every lane of a wave may hold a different
 // request kind, and a branchy body costs exec-mask juggling on all of them.
-__device__ __forceinline__ uint32_t acceptor_step(AccState& A, uint32_t kind, int32_t x, uint32_t z,
+// `live` = false makes the call a no-op (no state change, reply NONE), so the
+// batch kernel can run it predicated instead of under a branch.
+__device__ __forceinline__ uint32_t acceptor_step(AccState& A, bool live, uint32_t kind, int32_t x, uint32_t z,
                                                   int32_t& rx, int32_t& ry, uint32_t& rz,
                                                   uint32_t& exec_val) {
-  const bool is_ask = kind == ASK;                       // Server.hs:54
-  const bool is_prop = kind == PROPOSE;                  // Server.hs:64
-  const bool is_exec = kind == EXECUTE;                  // Server.hs:73
+  const bool is_ask = live && kind == ASK;               // Server.hs:54
+  const bool is_prop = live && kind == PROPOSE;          // Server.hs:64
+  const bool is_exec = live && kind == EXECUTE;          // Server.hs:73
   const bool grant = is_ask && !(A.t_max >= x);          // :56  T_max >= t -> HaveTicket
   const bool accept = is_prop && (x == A.t_max);         // :66  equality, not >=
   const bool hit = is_exec && (A.t_max == x);            // :75
   const bool panic = hit && A.val == 0u;                 // :76 `Just (_, c) <-` fails (Q6)
   const bool run = hit && A.val != 0u;                   // :77-78
-  const uint32_t rk = grant ? R1OK : accept ? R2S : (is_exec ? NONE : HAVE);
+  const uint32_t rk = grant ? R1OK : accept ? R2S : ((is_ask || is_prop) ? HAVE : NONE);
   rx = grant ? x : (accept ? 0 : A.t_max);               // :58/:71 HaveTicket T_max; :62 Round1OK t
   ry = grant ? A.t_store : 0;                            // :61-62 Round1OK t prop
   rz = grant ? A.val : 0u;
