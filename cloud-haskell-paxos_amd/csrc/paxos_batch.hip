@@ -161,6 +161,15 @@ template <int PM> struct Occ { static constexpr int waves = PXB_OCC_P1; };
 template <> struct Occ<2> { static constexpr int waves = PXB_OCC_P2; };
 template <> struct Occ<3> { static constexpr int waves = PXB_OCC_P3; };
 
+// Philox with its inputs made opaque, so the compiler cannot hoist the
+// per-instance half of the rounds (quarter-rate multiplies) out of the rare
+// fault branch into every step.
+__device__ __forceinline__ uint4 philox_here(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                             uint32_t k0, uint32_t k1) {
+  asm volatile("" : "+v"(c0), "+v"(c1), "+s"(k0), "+s"(k1));
+  return philox(c0, c1, c2, c3, k0, k1);
+}
+
 template <int PM, int N>
 __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KParams kp) {
   constexpr int G = 64 / N;
@@ -169,7 +178,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
   __shared__ Lds<PM, N> s_lds[WPB];
 
   const int lane = threadIdx.x & 63;
-  const int wib = threadIdx.x >> 6;
+  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   Lds<PM, N>& L = s_lds[wib];
   const int g = lane / N;
   const int a = lane - g * N;
@@ -215,7 +224,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
   uint32_t ca = 0, cb = 0, cc = 0, cd = 0, ce = 0, rounds_acc = 0, steps_acc = 0;
 #pragma unroll
   for (int p = 0; p < PM; ++p) {
-    S[p] = PropState{0, 0, 0, IDLE, 0, 0, 0, 0, false};
+    S[p] = PropState{0, 0, 0, IDLE, 0, 0, 0, 0, 0u};
     skew[p] = 0;
     R[p] = Link{0, 0, 0};
     Sx[p] = Link{0, 0, 0};
@@ -231,7 +240,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
     bool ok = true;
     if (pred && faulty) {
       const uint64_t inst = kp.first_instance + idx;
-      const uint4 w = philox((uint32_t)inst, (uint32_t)(inst >> 32), k, (1u << 24) | dirbits | (uint32_t)a, k0, k1);
+      const uint4 w = philox_here((uint32_t)inst, (uint32_t)(inst >> 32), k, (1u << 24) | dirbits | (uint32_t)a, k0, k1);
       ok = !(lossy && w.x <= loss_m1);
       d = 1 + (int32_t)mulhi_n(w.y, dmax);
     }
@@ -323,7 +332,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
           const uint32_t wp = (p == 0) ? wsk.x : (p == 1) ? wsk.y : wsk.z;
           skew[p] = (kp.skew_max > 0u) ? (int32_t)mulhi_n(wp, kp.skew_max + 1u) : 0;
           if ((uint32_t)p < P) last_tick = max(last_tick, skew[p]);
-          S[p] = PropState{0, 0, 0, IDLE, 0, 0, 0, 0, false};
+          S[p] = PropState{0, 0, 0, IDLE, 0, 0, 0, 0, 0u};
           R[p] = Link{0, 0, 0};
           Sx[p] = Link{0, 0, 0};
         });
@@ -533,6 +542,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
     const bool cap = active && !quiet && (s + 1 >= (int32_t)kp.step_cap);
     s += active ? 1 : 0;
     const bool done = quiet || cap;
+    STAMP(5);
     if (any(done)) {
       const uint32_t pan = slot(ballot(A.dead));             // Q6: dead <=> panicked
       const uint32_t dvg = slot(ballot((lflags & PXB_F_LOG_DIVERGENCE) != 0u));
@@ -579,10 +589,10 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
         active = false;
       }
     }
-    STAMP(5);
+    STAMP(6);
   }
 
-  STAMP(6);
+  STAMP(7);
   STAMP_FLUSH(kp.dbg);
   // ---------------- flush lane totals -----------------------------------------
   uint32_t v[13] = {ca & 0xFFFFu, ca >> 16, cb & 0xFFFFu, cb >> 16, cc & 0xFFFFu, cc >> 16,
@@ -633,7 +643,7 @@ __global__ void proposer_hook_kernel(pxb_proposer_rec* st, uint32_t n_acc, const
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= count) return;
   pxb_proposer_rec R = st[i];
-  PropState S{R.ticket, R.cmd, R.acks, R.state, R.mr_t, R.mr_v, R.r2_t, R.r2_v, R.pending != 0u};
+  PropState S{R.ticket, R.cmd, R.acks, R.state, R.mr_t, R.mr_v, R.r2_t, R.r2_v, R.pending != 0u ? 1u : 0u};
   Req o0{NONE, 0, 0}, o1{NONE, 0, 0};
   uint32_t no;
   if (in[i].kind == 3u)

@@ -97,7 +97,7 @@ struct PropState {
   uint32_t mr_v;
   int32_t r2_t;     // Round2State._proposal
   uint32_t r2_v;
-  bool pending;     // Round2State._originalCommandPending
+  uint32_t pending; // Round2State._originalCommandPending (0 / 1)
 };
 
 struct Req {
@@ -157,7 +157,7 @@ __device__ __forceinline__ uint32_t proposer_step(PropState& S, uint32_t n_acc, 
       }
       S.r2_t = x;                          // :157-167 (Q5: pending whenever mr is Just)
       S.r2_v = (mv == 0) ? S.cmd : mv;
-      S.pending = (mv != 0);
+      S.pending = (mv != 0) ? 1u : 0u;
       S.acks = 0;                          // :168
       S.rs = ROUND2;                       // :169
       S.mr_t = 0;

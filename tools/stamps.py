@@ -5,12 +5,12 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["PXB_LIB"] = os.path.join(ROOT, "variants", "stamps.so")
+os.environ.setdefault("PXB_LIB", os.path.join(ROOT, "variants", "stamps.so"))
 sys.path.insert(0, os.path.join(ROOT, "cloud-haskell-paxos_amd"))
 import torch  # noqa
 import pxb  # noqa
 
-NAMES = ["refill", "acceptor", "prop_tick+count", "prop_fast", "prop_serial+tail", "endstep+finish", "exit", "-"]
+NAMES = ["refill", "acceptor", "prop_tick+count", "prop_fast", "prop_serial+tail", "endstep", "finish", "exit"]
 lib = pxb.load()
 lib.pxb_debug_stamps.argtypes = [C.c_void_p]
 for c, n in ((2, 1 << 20), (3, 1 << 22), (5, 1 << 20)):
@@ -24,5 +24,5 @@ for c, n in ((2, 1 << 20), (3, 1 << 22), (5, 1 << 20)):
     lib.pxb_debug_stamps(C.cast(buf, C.c_void_p))
     total = sum(buf)
     steps = tot.cpu().tolist()[12] / 2
-    print("config %d: %s" % (c, "  ".join("%s %.1f%%" % (NAMES[i], 100.0 * buf[i] / total) for i in range(7))))
+    print("config %d: %s" % (c, "  ".join("%s %.1f%%" % (NAMES[i], 100.0 * buf[i] / total) for i in range(8))))
     print("   total wave-cycles %.3g, per instance-step %.1f" % (total, total / steps))
