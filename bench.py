@@ -187,6 +187,12 @@ def main():
             extra["config%d" % ec] = {"instances_per_step": en, "instances_per_s": ecnt["instances"] / es,
                                       "decided_per_s": ecnt["decided"] / es, "kernel_ms": ek,
                                       "counters": ecnt}
+        # log mode: stock Main.hs topology with the ticker running (SEMANTICS §9)
+        en = 1 << 20
+        es, ek, ecnt = run_workload(pxb.LOG_CONFIG, en, 2, 1, 0, 1, stream, dev)
+        extra["log_mode"] = {"instances_per_step": en, "ticks_per_proposer": pxb.LOG_CONFIG.n_ticks,
+                             "commands_committed_per_s": ecnt["executes"] / es,
+                             "instances_per_s": ecnt["instances"] / es, "kernel_ms": ek, "counters": ecnt}
         line["extra"] = extra
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)

@@ -74,6 +74,7 @@ struct KParams {
   uint32_t loss_m1, crash_m1;         // thr-1 (valid when LOSSY / CRASHY)
   uint32_t loss_ppm, crash_ppm;       // maxima for RANDOMIZE
   uint32_t crash_len_max, crash_start_max, skew_max, step_cap;
+  uint32_t n_ticks, tick_period;      // log mode (LOGM kernels): Ticks per proposer, spacing
   uint4* out;                         // pxb_result records (nullable)
   uint32_t* dig;
   uint4* acc;
@@ -147,14 +148,29 @@ __device__ __forceinline__ void l_pop_if(Link& L, bool p) {
   L.hl = p ? ((L.hl + 15u) & ~0x80u) : L.hl;
 }
 
-template <int PM, int N>
+// Log mode (several Ticks per proposer, SEMANTICS §9) carries full commands
+// "c<id>.<t>" (16 bits: id << 14 | t) instead of the single-decree clientId:
+// a Round1OK then needs a second word, kept in a parallel ring.
+template <int PM, bool LOGM> struct Ring2 { uint32_t w[PM][QD][64]; };
+template <int PM> struct Ring2<PM, false> { uint32_t w[1][1][1]; };
+
+template <int PM, int N, bool LOGM>
 struct Lds {
   static constexpr int G = 64 / N;
+  using clog_t = std::conditional_t<LOGM, unsigned long long, uint32_t>;
   uint32_t rq[PM][QD][64];       // links p -> a   (lane-interleaved: conflict-free)
   uint32_t sq[PM][QD][64];       // links a -> p
-  uint32_t clog[G][LT + 1];      // per-slot canonical log (+1 pad: rows on distinct banks);
-                                 // entries are (epoch << 2 | command), epoch = instance tag
+  clog_t clog[G][LT + 1];        // per-slot canonical log (+1 pad: rows on distinct banks);
+                                 // entries are (epoch << CB | command), epoch = instance tag
+  Ring2<PM, LOGM> sq2;           // links a -> p, command word (log mode)
 };
+
+// command word -> the result encoding (clientId << 24) | t of "c<id>.<t>"
+template <bool LOGM>
+__device__ __forceinline__ uint32_t code32(uint32_t v) {
+  if constexpr (LOGM) return v ? (((v >> 14) << 24) | (v & 0x3FFFu)) : 0u;
+  else return v ? ((v << 24) | 1u) : 0u;
+}
 
 // occupancy target (waves per SIMD) by proposer count: bounds the VGPR budget
 template <int PM> struct Occ { static constexpr int waves = PXB_OCC_P1; };
@@ -170,22 +186,27 @@ __device__ __forceinline__ uint4 philox_here(uint32_t c0, uint32_t c1, uint32_t 
   return philox(c0, c1, c2, c3, k0, k1);
 }
 
-template <int PM, int N>
+template <int PM, int N, bool LOGM>
 __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KParams kp) {
   constexpr int G = 64 / N;
   constexpr uint32_t NM = (1u << N) - 1u;     // slot-local lane mask
   constexpr uint32_t ENONE = 16u;             // "no event" acceptor index (N <= 9 < 16)
-  __shared__ Lds<PM, N> s_lds[WPB];
+  // command field of a request word: single decree = clientId (2 bits, t = 1),
+  // log mode = id << 14 | t (16 bits); the kind sits above it
+  constexpr uint32_t ZM = LOGM ? 0xFFFFu : 3u, KSH = LOGM ? 30u : 16u;
+  using clog_t = typename Lds<PM, N, LOGM>::clog_t;
+  constexpr uint32_t CB = LOGM ? 32u : 2u;    // epoch shift of a canonical-log entry
+  __shared__ Lds<PM, N, LOGM> s_lds[WPB];
 
   const int lane = threadIdx.x & 63;
   const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  Lds<PM, N>& L = s_lds[wib];
+  Lds<PM, N, LOGM>& L = s_lds[wib];
   const int g = lane / N;
   const int a = lane - g * N;
   const bool used = g < G;
   const int base = g * N;
   const uint32_t ltm = (1u << a) - 1u;        // slot-local lanes below me
-  uint32_t* clog = &L.clog[used ? g : 0][0];
+  clog_t* clog = &L.clog[used ? g : 0][0];
   for (int k = lane; k < G * (LT + 1); k += 64) (&L.clog[0][0])[k] = 0u;   // epoch 0 = empty
   // a ballot restricted to my slot, as an N-bit mask indexed by acceptor
   auto slot = [&](uint64_t b) -> uint32_t { return (uint32_t)(b >> base) & NM; };   // unused lanes never act
@@ -214,6 +235,9 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
   uint32_t canon = 0;                     // lane: canonical bytes of the current instance
   PropState S[PM];                        // replicated proposers (ClientState)
   int32_t skew[PM];
+  int32_t ntick[PM];                      // log mode: step of proposer p's next Tick
+  uint32_t tleft[PM];                     // log mode: Ticks still to come
+  uint32_t execs = 0, execs_acc = 0;      // Execute broadcasts (commands committed)
   Link R[PM], Sx[PM];                     // lane: links p -> a, a -> p
   uint32_t msgs_acc = 0;                  // lane totals across instances
   uint64_t canon_acc = 0;
@@ -226,13 +250,16 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
   for (int p = 0; p < PM; ++p) {
     S[p] = PropState{0, 0, 0, IDLE, 0, 0, 0, 0, 0u};
     skew[p] = 0;
+    ntick[p] = 0;
+    tleft[p] = 0;
     R[p] = Link{0, 0, 0};
     Sx[p] = Link{0, 0, 0};
   }
 
   // common link send, predicated on `pred` (docs/SEMANTICS.md §5): Philox
   // loss/delay, FIFO due, bounded ring (overflow -> flag, message dropped)
-  auto link_send = [&](Link& Lk, uint32_t* ring, uint32_t dirbits, uint32_t word, bool pred) {
+  auto link_send = [&](Link& Lk, uint32_t* ring, uint32_t* ring2, uint32_t dirbits, uint32_t word,
+                       uint32_t word2, bool pred) {
     msgs_acc += pred ? 1u : 0u;
     const uint32_t k = Lk.seq;
     Lk.seq = pred ? k + 1u : k;
@@ -250,7 +277,11 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
     const bool ovf = pred && ok && full;
     if (any(ovf)) lflags |= ovf ? (uint32_t)PXB_F_QUEUE_OVERFLOW : 0u;
     const int32_t due = max(s + d, l_last(Lk));
-    if (push) ring[((l_head(Lk) + len) & 7u) * 64u + (uint32_t)lane] = word;
+    if (push) {
+      const uint32_t at = ((l_head(Lk) + len) & 7u) * 64u + (uint32_t)lane;
+      ring[at] = word;
+      if (ring2) ring2[at] = word2;
+    }
     Lk.dn = push ? (Lk.dn | (((uint32_t)due & 15u) << (4u * len))) : Lk.dn;
     Lk.hl = push ? (((Lk.hl & 0x7Fu) + 1u) | ((uint32_t)due << 8)) : Lk.hl;
   };
@@ -258,10 +289,14 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
   auto send_req = [&](auto pc, bool has, uint32_t kind, int32_t x, uint32_t z) {
     constexpr int p = decltype(pc)::value;
     rounds += (has && kind == ASK) ? 1u : 0u;
-    const bool first_exec = has && kind == EXECUTE && dval == 0u;   // the decided value
-    dval = first_exec ? S[p].r2_v : dval;
-    dtick = first_exec ? x : dtick;
-    link_send(R[p], &L.rq[p][0][0], (uint32_t)p << 8, (uint32_t)x | (z << 14) | (kind << 16), has);
+    const bool ex = has && kind == EXECUTE;
+    if (any(ex)) {                      // a slot committed (Client.hs:178)
+      execs += ex ? 1u : 0u;
+      const bool first_exec = ex && dval == 0u;   // the decided value
+      dval = first_exec ? S[p].r2_v : dval;
+      dtick = first_exec ? x : dtick;
+    }
+    link_send(R[p], &L.rq[p][0][0], nullptr, (uint32_t)p << 8, (uint32_t)x | (z << 14) | (kind << KSH), 0u, has);
   };
   // one request from the head of link p -> a, predicated on `due`:
   // handleClientRequest, Server.hs:51-78 (dead / isolated acceptors discard it)
@@ -269,23 +304,23 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
     constexpr int p = decltype(pc)::value;
     const uint32_t w = L.rq[p][l_head(R[p])][lane];
     l_pop_if(R[p], due);
-    const uint32_t kind = (w >> 16) & 3u;
+    const uint32_t kind = (w >> KSH) & 3u;
     const bool live = due && !A.dead && !isolated;
     const uint32_t rb = 8u + ((kind & 1u) << 2);       // payload: Propose 12, Ask / Execute 8
     canon += live ? 2u * rb + 32u : (due ? rb : 0u);    // discarded: written, not read
     int32_t rx, ry;
     uint32_t rz, ev;
-    const uint32_t rk = acceptor_step(A, live, kind, (int32_t)(w & 0x3FFFu), (w >> 14) & 3u, rx, ry, rz, ev);
+    const uint32_t rk = acceptor_step(A, live, kind, (int32_t)(w & 0x3FFFu), (w >> 14) & ZM, rx, ry, rz, ev);
     if (any(ev != 0u)) {
       if (ev != 0u) {
-        digest = fnv_u32(digest, (ev << 24) | 1u);
+        digest = fnv_u32(digest, code32<LOGM>(ev));
         if (log_len < (uint32_t)LT) {
           // two acceptors of this instance executed different commands at
           // the same position iff the max already holds this epoch with
           // another command (order-independent, SEMANTICS §7)
-          const uint32_t tag = idx - first_idx + 1u;
-          const uint32_t old = atomicMax(&clog[log_len], (tag << 2) | ev);
-          if ((old >> 2) == tag && (old & 3u) != ev) lflags |= PXB_F_LOG_DIVERGENCE;
+          const clog_t tag = (clog_t)(idx - first_idx + 1u);
+          const clog_t old = atomicMax(&clog[log_len], (tag << CB) | (clog_t)ev);
+          if ((old >> CB) == tag && (uint32_t)(old & (((clog_t)1 << CB) - 1u)) != ev) lflags |= PXB_F_LOG_DIVERGENCE;
         } else {
           lflags |= PXB_F_LOG_TRUNC;
         }
@@ -293,8 +328,11 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
       }
     }
     // tickets are < 2^14 (SEMANTICS §6), so the fields need no masking
-    link_send(Sx[p], &L.sq[p][0][0], (1u << 16) | ((uint32_t)p << 8),
-              (uint32_t)rx | ((uint32_t)ry << 14) | (rz << 28) | (rk << 30), rk != NONE);
+    // (log mode: the clientId field says Just / Nothing, the full command
+    // travels in the second ring)
+    link_send(Sx[p], &L.sq[p][0][0], LOGM ? &L.sq2.w[p][0][0] : nullptr, (1u << 16) | ((uint32_t)p << 8),
+              (uint32_t)rx | ((uint32_t)ry << 14) | ((LOGM ? (rz >> 14) : rz) << 28) | (rk << 30), rz,
+              rk != NONE);
   };
 
   STAMP_DECL
@@ -331,7 +369,11 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
           constexpr int p = decltype(pc)::value;
           const uint32_t wp = (p == 0) ? wsk.x : (p == 1) ? wsk.y : wsk.z;
           skew[p] = (kp.skew_max > 0u) ? (int32_t)mulhi_n(wp, kp.skew_max + 1u) : 0;
-          if ((uint32_t)p < P) last_tick = max(last_tick, skew[p]);
+          ntick[p] = skew[p];
+          tleft[p] = kp.n_ticks;
+          // the last Tick: skew + (n_ticks - 1) * period (single decree: skew)
+          if ((uint32_t)p < P)
+            last_tick = max(last_tick, skew[p] + (LOGM ? (int32_t)((kp.n_ticks - 1u) * kp.tick_period) : 0));
           S[p] = PropState{0, 0, 0, IDLE, 0, 0, 0, 0, 0u};
           R[p] = Link{0, 0, 0};
           Sx[p] = Link{0, 0, 0};
@@ -350,7 +392,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
         log_len = lflags = 0;
         canon = 0;
         digest = 0x811C9DC5u;
-        rounds = dval = 0;
+        rounds = dval = execs = 0;
         dtick = 0;
         s = 0;
         active = true;
@@ -385,13 +427,22 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
       constexpr int p = decltype(pc)::value;
       const bool pact = active && (uint32_t)p < P;
       bool stepped = false;
-      const bool tick = pact && s == skew[p];
+      // the ticker (Client.hs:96-100): one Tick at skew_p (single decree), or
+      // n_ticks Ticks tick_period steps apart (log mode)
+      const bool tick = LOGM ? (pact && tleft[p] != 0u && s == ntick[p]) : (pact && s == skew[p]);
       if (any(tick)) {                          // handleTick, Client.hs:196-207
         Req o0{NONE, 0, 0};
         uint32_t no = 0;
         if (tick) {
-          no = proposer_tick(S[p], (uint32_t)(p + 1), o0);   // compact cmd = clientId (t = 1)
+          // command "c<id>.<t>" with t the new ticket (Client.hs:200-203);
+          // single decree: t = 1, carried as the clientId alone
+          const uint32_t cmd = LOGM ? (((uint32_t)(p + 1) << 14) | (uint32_t)(S[p].ticket + 1)) : (uint32_t)(p + 1);
+          no = proposer_tick(S[p], cmd, o0);
           stepped = true;
+          if (LOGM) {
+            ntick[p] += (int32_t)kp.tick_period;
+            tleft[p] -= 1u;
+          }
         }
         send_req(pc, no > 0u, o0.kind, o0.x, o0.z);
       }
@@ -415,11 +466,12 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
         if (any(fast)) {
           const bool has = fast && cnt_p == 1u;
           const uint32_t w = L.sq[p][l_head(Sx[p])][lane];
+          const uint32_t w2 = LOGM ? L.sq2.w[p][l_head(Sx[p])][lane] : 0u;
           l_pop_if(Sx[p], has);
           const uint32_t kind = has ? (w >> 30) : 3u;       // 3: no response
           const int32_t x = (int32_t)(w & 0x3FFFu);
           const int32_t y = (int32_t)((w >> 14) & 0x3FFFu);
-          const uint32_t z = has ? ((w >> 28) & 3u) : 0u;
+          const uint32_t z = has ? (LOGM ? w2 : ((w >> 28) & 3u)) : 0u;
           canon += has ? 2u * (16u >> kind) : 0u;
           uint32_t rem = slot(ballot(has));                 // unprocessed responses
           const uint32_t havem = slot(ballot(kind == HAVE));
@@ -509,12 +561,14 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
               const bool take = ca_ > 0u;
               const uint32_t mine = L.sq[p][l_head(Sx[p])][lane];
               const uint32_t w = (uint32_t)__shfl((int)mine, base + aa);
+              uint32_t z = (w >> 28) & 3u;
+              if (LOGM) z = (uint32_t)__shfl((int)L.sq2.w[p][l_head(Sx[p])][lane], base + aa);
               Req o0{NONE, 0, 0}, o1{NONE, 0, 0};
               uint32_t no = 0;
               if (take) {
                 const uint32_t kind = w >> 30;
                 no = proposer_step(S[p], (uint32_t)N, kind, (int32_t)(w & 0x3FFFu),
-                                   (int32_t)((w >> 14) & 0x3FFFu), (w >> 28) & 3u, o0, o1);
+                                   (int32_t)((w >> 14) & 0x3FFFu), z, o0, o1);
                 if (a == aa) canon += 2u * (16u >> kind);
                 l_pop_if(Sx[p], a == aa);
                 ca_--;
@@ -568,10 +622,11 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
           ce += (f & PXB_F_LOG_TRUNC) ? 1u : 0u;
           rounds_acc += rounds;
           steps_acc += (uint32_t)s;
+          execs_acc += execs;
         }
         if (a == 0 && kp.out) {
           uint4 r;
-          r.x = dval ? ((dval << 24) | 1u) : 0u;
+          r.x = code32<LOGM>(dval);
           r.y = dval ? (uint32_t)dtick : 0u;
           r.z = rounds;
           r.w = (f & 0xFFu) | ((uint32_t)s << 16);
@@ -582,7 +637,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
           uint4 r;
           r.x = (uint32_t)A.t_max;
           r.y = (uint32_t)A.t_store;
-          r.z = A.val ? ((A.val << 24) | 1u) : 0u;
+          r.z = code32<LOGM>(A.val);
           r.w = log_len | ((A.dead ? 1u : 0u) << 31);
           kp.acc[(uint64_t)idx * N + a] = r;
         }
@@ -595,29 +650,29 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
   STAMP(7);
   STAMP_FLUSH(kp.dbg);
   // ---------------- flush lane totals -----------------------------------------
-  uint32_t v[13] = {ca & 0xFFFFu, ca >> 16, cb & 0xFFFFu, cb >> 16, cc & 0xFFFFu, cc >> 16,
-                    cd & 0xFFFFu, cd >> 16, ce, rounds_acc, steps_acc, msgs_acc, 0u};
+  uint32_t v[14] = {ca & 0xFFFFu, ca >> 16, cb & 0xFFFFu, cb >> 16, cc & 0xFFFFu, cc >> 16,
+                    cd & 0xFFFFu, cd >> 16, ce, rounds_acc, steps_acc, msgs_acc, execs_acc, 0u};
   uint64_t c64 = canon_acc;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
 #pragma unroll
-    for (int q = 0; q < 12; ++q) v[q] += (uint32_t)__shfl_xor((int)v[q], off);
+    for (int q = 0; q < 13; ++q) v[q] += (uint32_t)__shfl_xor((int)v[q], off);
     const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)c64, off);
     const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(c64 >> 32), off);
     c64 += ((uint64_t)hi << 32) | lo;
   }
-  if (lane < 13) {
+  if (lane < 14) {
     // lane q adds counter q (one atomic per lane, no serialisation within the wave)
-    const int slot_of[13] = {PXB_C_INSTANCES, PXB_C_UNDECIDED, PXB_C_STUCK, PXB_C_PANIC, PXB_C_DIVERGENCE,
+    const int slot_of[14] = {PXB_C_INSTANCES, PXB_C_UNDECIDED, PXB_C_STUCK, PXB_C_PANIC, PXB_C_DIVERGENCE,
                              PXB_C_STEP_CAP, PXB_C_QUEUE_OVERFLOW, PXB_C_TICKET_OVERFLOW, PXB_C_LOG_TRUNC,
-                             PXB_C_ROUNDS, PXB_C_STEPS, PXB_C_MESSAGES, PXB_C_DECIDED};
+                             PXB_C_ROUNDS, PXB_C_STEPS, PXB_C_MESSAGES, PXB_C_EXECUTES, PXB_C_DECIDED};
     unsigned long long val = 0;
 #pragma unroll
-    for (int q = 0; q < 12; ++q) val = (lane == q) ? (unsigned long long)v[q] : val;
-    if (lane == 12) val = (unsigned long long)v[0] - (unsigned long long)v[1];   // decided
+    for (int q = 0; q < 13; ++q) val = (lane == q) ? (unsigned long long)v[q] : val;
+    if (lane == 13) val = (unsigned long long)v[0] - (unsigned long long)v[1];   // decided
     if (val) atomicAdd(&kp.totals[slot_of[lane]], val);
   }
-  if (lane == 13) atomicAdd(&kp.totals[PXB_C_CANON_BYTES], (unsigned long long)c64);
+  if (lane == 14) atomicAdd(&kp.totals[PXB_C_CANON_BYTES], (unsigned long long)c64);
 }
 
 // ---- single-handler hook kernels ------------------------------------------
@@ -660,29 +715,30 @@ __global__ void proposer_hook_kernel(pxb_proposer_rec* st, uint32_t n_acc, const
 // ---- host side ----------------------------------------------------------------
 typedef void (*kernel_fn)(KParams);
 
-template <int PM, int N>
-static kernel_fn kfn() { return paxos_batch_kernel<PM, N>; }
+template <int PM, int N, bool LOGM>
+static kernel_fn kfn() { return paxos_batch_kernel<PM, N, LOGM>; }
 
-template <int PM>
+template <int PM, bool LOGM>
 static kernel_fn pick_n(uint32_t n) {
   switch (n) {
-    case 2: return kfn<PM, 2>();
-    case 3: return kfn<PM, 3>();
-    case 4: return kfn<PM, 4>();
-    case 5: return kfn<PM, 5>();
-    case 6: return kfn<PM, 6>();
-    case 7: return kfn<PM, 7>();
-    case 8: return kfn<PM, 8>();
-    case 9: return kfn<PM, 9>();
+    case 2: return kfn<PM, 2, LOGM>();
+    case 3: return kfn<PM, 3, LOGM>();
+    case 4: return kfn<PM, 4, LOGM>();
+    case 5: return kfn<PM, 5, LOGM>();
+    case 6: return kfn<PM, 6, LOGM>();
+    case 7: return kfn<PM, 7, LOGM>();
+    case 8: return kfn<PM, 8, LOGM>();
+    case 9: return kfn<PM, 9, LOGM>();
   }
   return nullptr;
 }
 
-static kernel_fn pick(uint32_t pm, uint32_t n) {
+// single decree (one Tick per proposer) or log mode (several)
+static kernel_fn pick(uint32_t pm, uint32_t n, bool logm) {
   switch (pm) {
-    case 1: return pick_n<1>(n);
-    case 2: return pick_n<2>(n);
-    case 3: return pick_n<3>(n);
+    case 1: return logm ? pick_n<1, true>(n) : pick_n<1, false>(n);
+    case 2: return logm ? pick_n<2, true>(n) : pick_n<2, false>(n);
+    case 3: return logm ? pick_n<3, true>(n) : pick_n<3, false>(n);
   }
   return nullptr;
 }
@@ -692,7 +748,7 @@ static thread_local int g_last_hip = 0;
 static unsigned long long* g_dbg = nullptr;
 #endif
 static std::mutex g_mu;
-static int g_occ[4][10][64];            // [pm][n][device] blocks per CU (0 = unknown)
+static int g_occ[2][4][10][64];         // [logm][pm][n][device] blocks per CU (0 = unknown)
 static int g_cus[64];
 
 static int hip_fail(hipError_t e) {
@@ -715,6 +771,8 @@ static int validate(const pxb_config* c) {
   if (c->skew_max > 4096) return PXB_E_INVAL;
   if (c->step_cap < 1 || c->step_cap > PXB_MAX_STEP_CAP) return PXB_E_INVAL;
   if (c->n_instances > (1ull << 40)) return PXB_E_INVAL;
+  if (c->n_ticks > PXB_MAX_TICKS) return PXB_E_INVAL;
+  if (c->n_ticks > 1 && (c->tick_period < 1 || c->tick_period > PXB_MAX_STEP_CAP)) return PXB_E_INVAL;
   return PXB_OK;
 }
 
@@ -761,7 +819,8 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
   int dev = 0;
   HIPCHK(hipGetDevice(&dev));
   if (dev < 0 || dev >= 64) return PXB_E_NODEV;
-  kernel_fn fn = pick(cfg->n_proposers, cfg->n_acceptors);
+  const bool logm = cfg->n_ticks > 1;   // log mode: several Ticks per proposer
+  kernel_fn fn = pick(cfg->n_proposers, cfg->n_acceptors, logm);
   if (!fn) return PXB_E_INVAL;
   const hipStream_t st = (hipStream_t)stream;
   int occ, cus;
@@ -772,7 +831,7 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
       HIPCHK(hipGetDeviceProperties(&prop, dev));
       g_cus[dev] = prop.multiProcessorCount;
     }
-    int& o = g_occ[cfg->n_proposers][cfg->n_acceptors][dev];
+    int& o = g_occ[logm ? 1 : 0][cfg->n_proposers][cfg->n_acceptors][dev];
     if (!o) {
       int nb = 0;
       HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)fn, BLOCK, 0));
@@ -795,6 +854,8 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
   kp.crash_start_max = cfg->crash_start_max;
   kp.skew_max = cfg->skew_max;
   kp.step_cap = cfg->step_cap;
+  kp.n_ticks = logm ? cfg->n_ticks : 1u;
+  kp.tick_period = logm ? cfg->tick_period : 1u;
   const uint64_t lt = prob_threshold(cfg->loss_ppm), ct = prob_threshold(cfg->crash_ppm);
   kp.cfg = ((cfg->flags & PXB_CFG_RANDOMIZE) ? CFG_RANDOMIZE : 0u) | (lt ? CFG_LOSSY : 0u) | (ct ? CFG_CRASHY : 0u);
   kp.loss_m1 = (uint32_t)(lt - 1ull);

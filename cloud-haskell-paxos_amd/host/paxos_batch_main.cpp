@@ -9,6 +9,7 @@
 // The Haskell binding of the same entry points is hs/PaxosBatch.hs.
 //
 //   paxos_batch_main [--config K] [--instances N] [--first F] [--gpus G] [--show S]
+//                    [--ticks T --period D]   (log mode: T Ticks per proposer, D steps apart)
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -56,7 +57,7 @@ static std::string flag_names(uint32_t f) {
 }
 
 int main(int argc, char** argv) {
-  int cfg_id = 2, gpus = 1, show = 4;
+  int cfg_id = 2, gpus = 1, show = 4, ticks = 0, period = 8;
   long long instances = -1, first = 0;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
@@ -66,11 +67,23 @@ int main(int argc, char** argv) {
     else if (a == "--first") first = atoll(next());
     else if (a == "--gpus") gpus = atoi(next());
     else if (a == "--show") show = atoi(next());
-    else { fprintf(stderr, "usage: %s [--config K] [--instances N] [--first F] [--gpus G] [--show S]\n", argv[0]); return 2; }
+    else if (a == "--ticks") ticks = atoi(next());      // log mode: Ticks per proposer
+    else if (a == "--period") period = atoi(next());    // steps between Ticks
+    else {
+      fprintf(stderr, "usage: %s [--config K] [--instances N] [--first F] [--gpus G] [--show S] "
+              "[--ticks T --period D]\n", argv[0]);
+      return 2;
+    }
   }
   pxb_config cfg = named_config(cfg_id);
   if (instances >= 0) cfg.n_instances = (uint64_t)instances;
   cfg.first_instance = (uint64_t)first;
+  if (ticks > 1) {
+    cfg.n_ticks = (uint32_t)ticks;
+    cfg.tick_period = (uint32_t)period;
+    const uint32_t need = (uint32_t)(ticks - 1) * (uint32_t)period + 64u;
+    if (cfg.step_cap < need) cfg.step_cap = need > PXB_MAX_STEP_CAP ? PXB_MAX_STEP_CAP : need;
+  }
   const uint64_t n = cfg.n_instances, N = cfg.n_acceptors;
   std::vector<pxb_result> res(n);
   std::vector<uint32_t> dig(n * N);
@@ -89,8 +102,8 @@ int main(int argc, char** argv) {
          gpus, dt);
   static const char* cn[PXB_NCOUNTERS] = {"decided", "undecided", "stuck", "panic", "divergence", "step_cap",
                                           "rounds", "messages", "queue_overflow", "ticket_overflow", "log_trunc",
-                                          "canon_bytes", "steps", "instances", "-", "-"};
-  for (int k = 0; k < 14; ++k) printf("  %-16s %lld\n", cn[k], (long long)tot.c[k]);
+                                          "canon_bytes", "steps", "instances", "executes", "-"};
+  for (int k = 0; k < 15; ++k) printf("  %-16s %lld\n", cn[k], (long long)tot.c[k]);
   for (uint64_t i = 0; i < n && i < (uint64_t)show; ++i) {
     const pxb_result& r = res[i];
     printf("instance %llu: decided %s @ Ticket %d, rounds %u, steps %u, flags %s, log digests",

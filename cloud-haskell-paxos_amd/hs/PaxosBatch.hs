@@ -17,6 +17,7 @@
 -- capabilities keep running meanwhile.
 module PaxosBatch
   ( BatchConfig (..)
+  , logConfig
   , Outcome (..)
   , Flag (..)
   , Totals (..)
@@ -41,7 +42,7 @@ import           Foreign.Marshal.Utils (with)
 import           Foreign.Ptr           (Ptr, nullPtr)
 import           Foreign.Storable      (Storable (..))
 
--- | pxb_config (64 bytes, see include/paxos_batch.h).
+-- | pxb_config (72 bytes, ABI 2, see include/paxos_batch.h).
 data BatchConfig = BatchConfig
   { bcSeed          :: !Word64
   , bcFirst         :: !Word64   -- ^ global id of the first instance
@@ -56,17 +57,20 @@ data BatchConfig = BatchConfig
   , bcSkewMax       :: !Word32
   , bcStepCap       :: !Word32
   , bcFlags         :: !Word32
+  , bcTicks         :: !Word32   -- ^ log mode: Ticks per proposer (<= 1: single decree);
+                                 --   the reference ticks forever (Client.hs:96-100)
+  , bcTickPeriod    :: !Word32   -- ^ steps between Ticks
   } deriving (Show)
 
 instance Storable BatchConfig where
-  sizeOf _ = 64
+  sizeOf _ = 72
   alignment _ = 8
   peek p = BatchConfig
     <$> peekByteOff p 0  <*> peekByteOff p 8  <*> peekByteOff p 16
     <*> peekByteOff p 24 <*> peekByteOff p 28 <*> peekByteOff p 32
     <*> peekByteOff p 36 <*> peekByteOff p 40 <*> peekByteOff p 44
     <*> peekByteOff p 48 <*> peekByteOff p 52 <*> peekByteOff p 56
-    <*> peekByteOff p 60
+    <*> peekByteOff p 60 <*> peekByteOff p 64 <*> peekByteOff p 68
   poke p c = do
     pokeByteOff p 0  (bcSeed c);        pokeByteOff p 8  (bcFirst c)
     pokeByteOff p 16 (bcCount c);       pokeByteOff p 24 (bcProposers c)
@@ -74,11 +78,17 @@ instance Storable BatchConfig where
     pokeByteOff p 36 (bcDelayMax c);    pokeByteOff p 40 (bcCrashPpm c)
     pokeByteOff p 44 (bcCrashLenMax c); pokeByteOff p 48 (bcCrashStartMax c)
     pokeByteOff p 52 (bcSkewMax c);     pokeByteOff p 56 (bcStepCap c)
-    pokeByteOff p 60 (bcFlags c)
+    pokeByteOff p 60 (bcFlags c);       pokeByteOff p 64 (bcTicks c)
+    pokeByteOff p 68 (bcTickPeriod c)
 
 -- | The stock topology of app/Main.hs (2 acceptors, 2 proposers), fault-free.
 defaultConfig :: BatchConfig
-defaultConfig = BatchConfig 0x5EED0001 0 1 2 2 0 1 0 1 0 0 256 0
+defaultConfig = BatchConfig 0x5EED0001 0 1 2 2 0 1 0 1 0 0 256 0 1 1
+
+-- | The stock app/Main.hs run as the reference does it: both clients keep
+-- ticking (here 16 Ticks, 8 steps apart), so the acceptor logs grow.
+logConfig :: BatchConfig
+logConfig = defaultConfig { bcTicks = 16, bcTickPeriod = 8, bcStepCap = 1024 }
 
 -- | BASELINE config 2: 2^20 instances, 1 proposer, 5 acceptors, no faults.
 config2 :: BatchConfig
@@ -102,7 +112,8 @@ data Outcome = Outcome
 -- | Run totals (pxb_counters, slots of SURVEY.md §8(e)).
 data Totals = Totals
   { tDecided, tUndecided, tStuck, tPanic, tDivergence, tStepCap
-  , tRounds, tMessages :: !Int64
+  , tRounds, tMessages
+  , tExecutes :: !Int64           -- ^ Execute broadcasts: commands committed (log mode)
   } deriving (Show)
 
 -- | "c<clientId>.<t>" from the command code (Client.hs:202-203).
@@ -142,8 +153,9 @@ runWith cfg call = do
             outs <- forM [0 .. n - 1] $ \i -> do
               [v, t, r, f] <- peekArray 4 (advancePtr pres (4 * i))
               pure (decode v t r f)
-            [d, u, s, p, dv, sc, rd, ms] <- peekArray 8 ptot
-            pure (Right (outs, Totals d u s p dv sc rd ms))
+            tot <- peekArray 16 ptot
+            let [d, u, s, p, dv, sc, rd, ms] = take 8 tot
+            pure (Right (outs, Totals d u s p dv sc rd ms (tot !! 14)))
 
 decode :: Word32 -> Word32 -> Word32 -> Word32 -> Outcome
 decode v t r f = Outcome

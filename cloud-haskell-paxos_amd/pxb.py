@@ -25,7 +25,7 @@ LIB_PATH = os.environ.get("PXB_LIB") or os.path.join(_HERE, "csrc", "libpaxos_ba
 # ---- constants (include/paxos_batch.h) ------------------------------------
 PXB_OK, PXB_E_INVAL, PXB_E_HIP, PXB_E_OOM, PXB_E_NODEV, PXB_E_RCCL = 0, -1, -2, -3, -4, -5
 MAX_PROPOSERS, MIN_ACCEPTORS, MAX_ACCEPTORS = 3, 2, 9
-MAX_DELAY, MAX_STEP_CAP, QUEUE_DEPTH, LOG_TRACK = 15, 8192, 8, 32
+MAX_DELAY, MAX_STEP_CAP, QUEUE_DEPTH, LOG_TRACK, MAX_TICKS = 15, 8192, 8, 32, 4096
 CFG_RANDOMIZE = 1
 
 F_UNDECIDED, F_STUCK, F_PANIC, F_LOG_DIVERGENCE = 1, 2, 4, 8
@@ -38,7 +38,7 @@ FLAG_NAMES = {F_UNDECIDED: "UNDECIDED", F_STUCK: "STUCK", F_PANIC: "PANIC",
 NCOUNTERS = 16
 COUNTER_NAMES = ["decided", "undecided", "stuck", "panic", "divergence", "step_cap",
                  "rounds", "messages", "queue_overflow", "ticket_overflow", "log_trunc",
-                 "canon_bytes", "steps", "instances", "reserved14", "reserved15"]
+                 "canon_bytes", "steps", "instances", "executes", "reserved15"]
 
 # ClientRequest (Common.hs:41-45) / ServerResponse (Common.hs:49-53) tags
 AskForTicket, Propose, Execute = 0, 1, 2
@@ -54,7 +54,8 @@ class pxb_config(C.Structure):
                 ("n_acceptors", C.c_uint32), ("loss_ppm", C.c_uint32),
                 ("delay_max", C.c_uint32), ("crash_ppm", C.c_uint32),
                 ("crash_len_max", C.c_uint32), ("crash_start_max", C.c_uint32),
-                ("skew_max", C.c_uint32), ("step_cap", C.c_uint32), ("flags", C.c_uint32)]
+                ("skew_max", C.c_uint32), ("step_cap", C.c_uint32), ("flags", C.c_uint32),
+                ("n_ticks", C.c_uint32), ("tick_period", C.c_uint32)]
 
 
 class pxb_result(C.Structure):
@@ -82,7 +83,7 @@ class pxb_proposer_rec(C.Structure):
                 ("client_id", C.c_uint32)]
 
 
-assert C.sizeof(pxb_config) == 64 and C.sizeof(pxb_result) == 16
+assert C.sizeof(pxb_config) == 72 and C.sizeof(pxb_result) == 16
 assert C.sizeof(pxb_acceptor_rec) == 16 and C.sizeof(pxb_msg) == 16
 
 # ---- Common.hs vocabulary ------------------------------------------------
@@ -118,12 +119,15 @@ class Config:
     skew_max: int = 0
     step_cap: int = 256
     randomize: bool = False
+    n_ticks: int = 1          # log mode when > 1: Ticks per proposer (Client.hs:96-100)
+    tick_period: int = 1      # steps between Ticks
 
     def to_c(self, first_instance: int, n_instances: int) -> pxb_config:
         return pxb_config(self.seed, first_instance, n_instances, self.n_proposers,
                           self.n_acceptors, self.loss_ppm, self.delay_max, self.crash_ppm,
                           self.crash_len_max, self.crash_start_max, self.skew_max,
-                          self.step_cap, CFG_RANDOMIZE if self.randomize else 0)
+                          self.step_cap, CFG_RANDOMIZE if self.randomize else 0,
+                          self.n_ticks, self.tick_period)
 
 
 CONFIGS = {
@@ -138,6 +142,13 @@ CONFIGS = {
               skew_max=3, step_cap=512, randomize=True),
 }
 CONFIG_INSTANCES = {1: 1 << 10, 2: 1 << 20, 3: 1 << 24, 4: 1 << 26, 5: 1 << 28}
+
+# Log mode (docs/SEMANTICS.md §9): the stock app/Main.hs
+# topology (2 proposers, 2 acceptors, Main.hs:41-46) with the ticker running
+# (Client.hs:96-100): 16 Ticks per proposer, 8 steps apart.
+LOG_CONFIG = Config(seed=0x5EED0006, n_proposers=2, n_acceptors=2, step_cap=1024,
+                    n_ticks=16, tick_period=8)
+CONFIGS[6] = LOG_CONFIG
 
 
 def canonical_bytes_nofault(n_acceptors: int) -> int:

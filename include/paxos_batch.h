@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PXB_ABI_VERSION 1
+#define PXB_ABI_VERSION 2
 
 /* ---- error codes ---------------------------------------------------------- */
 #define PXB_OK          0
@@ -45,6 +45,7 @@ extern "C" {
 #define PXB_QUEUE_DEPTH     8    /* messages per directed link              */
 #define PXB_LOG_TRACK      32    /* log positions checked for divergence    */
 #define PXB_TICKET_LIMIT (1 << 15)
+#define PXB_MAX_TICKS    4096    /* log mode: Ticks per proposer            */
 
 /* pxb_config.flags */
 #define PXB_CFG_RANDOMIZE 1u     /* config-5 fuzz: per-instance P, loss, delay,
@@ -68,6 +69,13 @@ typedef struct pxb_config {
   uint32_t skew_max;         /* proposer Tick step uniform in [0, skew_max]   */
   uint32_t step_cap;         /* 1..8192                                        */
   uint32_t flags;            /* PXB_CFG_*                                      */
+  /* log mode (ABI 2): the reference's ticker sends a Tick every second,
+   * forever (Client.hs:96-100).  n_ticks <= 1 = single decree (one Tick per
+   * proposer, at its skew step); n_ticks > 1 = proposer p gets Ticks at steps
+   * skew_p + j * tick_period, j = 0..n_ticks-1, and the acceptor logs grow one
+   * command per committed slot (Server.hs:73-78). */
+  uint32_t n_ticks;          /* 0 / 1 = single decree, else 2..PXB_MAX_TICKS   */
+  uint32_t tick_period;      /* steps between Ticks (log mode), 1..8192        */
 } pxb_config;
 
 /* Per-instance outcome (16 B).  decided_val is the Command of the first
@@ -107,7 +115,9 @@ enum {
   PXB_C_DIVERGENCE, PXB_C_STEP_CAP, PXB_C_ROUNDS, PXB_C_MESSAGES,
   PXB_C_QUEUE_OVERFLOW, PXB_C_TICKET_OVERFLOW, PXB_C_LOG_TRUNC,
   PXB_C_CANON_BYTES,         /* SURVEY.md §8(d) canonical accounting v1       */
-  PXB_C_STEPS, PXB_C_INSTANCES, PXB_C_RESERVED14, PXB_C_RESERVED15
+  PXB_C_STEPS, PXB_C_INSTANCES,
+  PXB_C_EXECUTES,            /* Execute broadcasts (commands committed)       */
+  PXB_C_RESERVED15
 };
 typedef struct pxb_counters { int64_t c[PXB_NCOUNTERS]; } pxb_counters;
 

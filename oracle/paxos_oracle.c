@@ -95,7 +95,7 @@ typedef struct {
   link_t rsp[MAXN][MAXP];
   uint32_t canon_log[PXB_LOG_TRACK];
   uint32_t flags, rounds;
-  uint64_t messages, canon;
+  uint64_t messages, canon, executes;
   int decided;
   uint32_t decided_val; int32_t decided_ticket;
 } inst_t;
@@ -221,6 +221,7 @@ static int proposer_handle(prop_t* pr, int N, const msg_t* m, msg_t out[2]) {
 static void bcast(inst_t* I, int p, int s, const msg_t* out, int nout) {
   for (int i = 0; i < nout; ++i) {
     if (out[i].kind == ASK) I->rounds++;
+    if (out[i].kind == EXECUTE) I->executes++;
     if (out[i].kind == EXECUTE && !I->decided) {
       I->decided = 1; I->decided_val = I->prop[p].r2_v; I->decided_ticket = out[i].x;
     }
@@ -258,6 +259,11 @@ static void run_instance(const pxb_config* cfg, uint64_t inst, pxb_result* res,
       if (I->skew[p] > last_tick) last_tick = I->skew[p];
     }
   }
+  /* ticker (Client.hs:96-100): n_ticks Ticks tick_period steps apart from
+   * skew_p (single decree: n_ticks <= 1, one Tick at skew_p) — SEMANTICS §9 */
+  const int n_ticks = cfg->n_ticks > 1 ? (int)cfg->n_ticks : 1;
+  const int period = cfg->n_ticks > 1 ? (int)cfg->tick_period : 1;
+  last_tick += (n_ticks - 1) * period;
   for (int a = 0; a < I->N; ++a) { I->acc[a].digest = 0x811C9DC5u; }
   if (crash_ppm > 0) {
     uint64_t thr = prob_threshold(crash_ppm);
@@ -303,7 +309,8 @@ static void run_instance(const pxb_config* cfg, uint64_t inst, pxb_result* res,
     for (int p = 0; p < P; ++p) {
       prop_t* pr = &I->prop[p];
       int active = 0;
-      if (s == I->skew[p]) {
+      const int since = s - I->skew[p];
+      if (since >= 0 && since % period == 0 && since / period < n_ticks) {
         active = 1;
         int n = proposer_tick(pr, out);
         bcast(I, p, s, out, n);
@@ -362,6 +369,7 @@ static void run_instance(const pxb_config* cfg, uint64_t inst, pxb_result* res,
   cnt[PXB_C_CANON_BYTES] += (int64_t)I->canon;
   cnt[PXB_C_STEPS] += steps;
   cnt[PXB_C_INSTANCES] += 1;
+  cnt[PXB_C_EXECUTES] += (int64_t)I->executes;
 }
 
 /* ---- threaded batch runner -------------------------------------------- */
@@ -392,6 +400,8 @@ int pxb_oracle_validate(const pxb_config* c) {
   if (c->crash_len_max < 1 || c->crash_len_max > 4096 || c->crash_start_max > 65535) return PXB_E_INVAL;
   if (c->skew_max > 4096) return PXB_E_INVAL;
   if (c->step_cap < 1 || c->step_cap > PXB_MAX_STEP_CAP) return PXB_E_INVAL;
+  if (c->n_ticks > PXB_MAX_TICKS) return PXB_E_INVAL;
+  if (c->n_ticks > 1 && (c->tick_period < 1 || c->tick_period > PXB_MAX_STEP_CAP)) return PXB_E_INVAL;
   return PXB_OK;
 }
 

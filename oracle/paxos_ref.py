@@ -376,6 +376,8 @@ class Config:
     skew_max: int = 0
     step_cap: int = 256
     randomize: bool = False   # config-5 fuzz: per-instance P/loss/delay/crash
+    n_ticks: int = 1          # log mode when > 1 (docs/SEMANTICS.md §9)
+    tick_period: int = 1      # steps between a proposer's Ticks
 
 
 @dataclass
@@ -429,6 +431,7 @@ class InstanceResult:
     acceptors: List[Acceptor]
     proposers: List[Proposer]
     max_queue: int
+    executes: int = 0       # Execute broadcasts (commands committed)
 
     def digest(self, a: int) -> int:
         acc = self.acceptors[a]
@@ -469,7 +472,12 @@ def run_instance(cfg: Config, inst: int, queue_depth: int = QUEUE_DEPTH,
     decided = None
     max_queue = 0
     canon_log = [NOTHING] * log_track
-    last_tick = max(prm.skew)
+    # the ticker (Client.hs:96-100): one Tick at skew_p (single decree) or
+    # n_ticks Ticks tick_period steps apart (log mode, docs/SEMANTICS.md §9)
+    n_ticks = max(1, cfg.n_ticks)
+    period = cfg.tick_period if n_ticks > 1 else 1
+    last_tick = max(prm.skew) + (n_ticks - 1) * period
+    executes = 0
     faulty = prm.loss_thr > 0 or prm.delay_max > 1
 
     def send(link: _Link, s: int, dirn: int, p: int, a: int, msg):
@@ -492,10 +500,12 @@ def run_instance(cfg: Config, inst: int, queue_depth: int = QUEUE_DEPTH,
         max_queue = max(max_queue, len(link.q))
 
     def bcast(p: int, s: int, out):
-        nonlocal rounds, decided
+        nonlocal rounds, decided, executes
         for (kind, ticket, val) in out:
             if kind == ASK:
                 rounds += 1
+            if kind == EXECUTE:
+                executes += 1
             if kind == EXECUTE and decided is None:
                 decided = (props[p].r2_v, ticket)
             for a in range(N):
@@ -536,7 +546,8 @@ def run_instance(cfg: Config, inst: int, queue_depth: int = QUEUE_DEPTH,
         for p in range(P):
             pr = props[p]
             active = False
-            if s == prm.skew[p]:
+            since = s - prm.skew[p]
+            if since >= 0 and since % period == 0 and since // period < n_ticks:
                 active = True
                 bcast(p, s, proposer_tick(pr))
             for a in range(N):
@@ -562,7 +573,8 @@ def run_instance(cfg: Config, inst: int, queue_depth: int = QUEUE_DEPTH,
         flags |= F_STUCK
     canon += 16 + 4 * N
     dv, dt = decided if decided else (NOTHING, 0)
-    return InstanceResult(dv, dt, rounds, flags, steps, messages, canon, accs, props, max_queue)
+    return InstanceResult(dv, dt, rounds, flags, steps, messages, canon, accs, props, max_queue,
+                          executes)
 
 
 def run_batch(cfg: Config, first: int, count: int, **kw) -> List[InstanceResult]:
@@ -585,4 +597,7 @@ def config(n: int) -> Config:
         return Config(seed=0x5EED0005, n_proposers=3, n_acceptors=9, loss_ppm=300000,
                       delay_max=8, crash_ppm=200000, crash_len_max=16, crash_start_max=16,
                       skew_max=3, step_cap=512, randomize=True)
+    if n == 6:   # log mode (docs/SEMANTICS.md §9): stock Main.hs topology, ticker running
+        return Config(seed=0x5EED0006, n_proposers=2, n_acceptors=2, step_cap=1024,
+                      n_ticks=16, tick_period=8)
     raise ValueError(n)

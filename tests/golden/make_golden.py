@@ -16,7 +16,8 @@ sys.path.insert(0, os.path.join(HERE, "..", "..", "oracle"))
 import paxos_ref as R  # noqa: E402
 
 # (config, first_instance, count): small enough for pure Python in seconds
-CASES = [(1, 0, 64), (2, 0, 64), (3, 0, 400), (3, (1 << 32) - 50, 100), (4, 0, 200), (5, 0, 300)]
+CASES = [(1, 0, 64), (2, 0, 64), (3, 0, 400), (3, (1 << 32) - 50, 100), (4, 0, 200), (5, 0, 300),
+         (6, 0, 200)]
 
 
 def main():

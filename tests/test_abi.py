@@ -42,9 +42,9 @@ def test_struct_layout_matches_header():
 #include <stddef.h>
 #include "paxos_batch.h"
 int main(void) {
-  printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(pxb_config), sizeof(pxb_result),
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(pxb_config), sizeof(pxb_result),
          sizeof(pxb_acceptor_rec), sizeof(pxb_counters), sizeof(pxb_msg), sizeof(pxb_proposer_rec),
-         offsetof(pxb_config, step_cap));
+         offsetof(pxb_config, step_cap), offsetof(pxb_config, tick_period));
   return 0;
 }'''
     tmp = "/tmp/pxb_layout"
@@ -54,12 +54,12 @@ int main(void) {
     got = [int(x) for x in subprocess.run([tmp], capture_output=True, text=True).stdout.split()]
     assert got == [C.sizeof(pxb.pxb_config), C.sizeof(pxb.pxb_result), C.sizeof(pxb.pxb_acceptor_rec),
                    C.sizeof(pxb.pxb_counters), C.sizeof(pxb.pxb_msg), C.sizeof(pxb.pxb_proposer_rec),
-                   pxb.pxb_config.step_cap.offset]
+                   pxb.pxb_config.step_cap.offset, pxb.pxb_config.tick_period.offset]
 
 
 def test_misc_entry_points_without_gpu():
     lib = pxb.load()
-    assert lib.pxb_abi_version() == 1
+    assert lib.pxb_abi_version() == 2
     assert lib.pxb_strerror(pxb.PXB_E_INVAL) == b"invalid argument"
     assert lib.pxb_canonical_bytes_nofault(5) == 1140
 

@@ -66,6 +66,34 @@ def test_edge_schedules(gpu_lib, kw):
     _cmp(pxb.Config(**base), 0, 2000)
 
 
+# ---- log mode (docs/SEMANTICS.md §9): periodic Ticks, Execute-driven slots -------
+@pytest.mark.parametrize("P,N,loss,delay,ticks,period,crash", [
+    (1, 5, 0, 1, 8, 6, 0),            # every Tick commits (period > one slot)
+    (1, 3, 0, 1, 6, 2, 0),            # Ticks while busy are dropped
+    (2, 5, 50000, 3, 6, 9, 0),        # duelling proposers, Q5 re-proposals in the log
+    (3, 7, 150000, 4, 5, 20, 150000),
+    (2, 9, 0, 6, 12, 5, 300000),
+    (3, 4, 300000, 8, 16, 3, 0)])
+def test_log_mode_matches_oracle(gpu_lib, P, N, loss, delay, ticks, period, crash):
+    cfg = pxb.Config(seed=0x1060 + 16 * P + N, n_proposers=P, n_acceptors=N, loss_ppm=loss,
+                     delay_max=delay, skew_max=3, crash_ppm=crash, crash_len_max=12,
+                     crash_start_max=30, step_cap=1024, n_ticks=ticks, tick_period=period)
+    res, cnt = _cmp(cfg, 321, 4001)
+    assert cnt["executes"] >= cnt["decided"]
+
+
+def test_log_mode_full_size_properties(gpu_lib):
+    """Fault-free log mode at 2^20 instances: every one of the 8 Ticks commits
+    its own command, so every acceptor log is c1.1 .. c1.8."""
+    cfg = pxb.Config(seed=0x5EED0006, n_proposers=1, n_acceptors=5, n_ticks=8, tick_period=6)
+    n = 1 << 20
+    res, dig, _, cnt = pxb.run(cfg, 0, n)
+    assert cnt["executes"] == 8 * n and cnt["rounds"] == 8 * n and cnt["decided"] == n
+    assert (res[:, 3] == ((7 * 6 + 6) << 16)).all()
+    _, edig, _, _ = oracle_c.run_cpu(cfg, 0, 1)
+    assert (dig == edig[0]).all()
+
+
 @pytest.mark.parametrize("n", [1, 7, 63, 64, 65, 1000])
 def test_ragged_batch_sizes(gpu_lib, n):
     _cmp(pxb.CONFIGS[3], 5, n)

@@ -146,6 +146,59 @@ def test_agreement_without_loss_single_proposer():
         assert not (r.flags & R.F_LOG_DIVERGENCE)
 
 
+# ---- log mode (docs/SEMANTICS.md §9): the reference's periodic ticker -------------
+def test_log_mode_each_tick_commits_a_new_slot():
+    """Client.hs:96-100 ticks a proposer forever; with ticks far enough apart
+    every Tick finds it Idle (Client.hs:199), starts "c1.<t>" at the next
+    ticket (Client.hs:200-203) and the acceptors log one command per slot."""
+    cfg = R.Config(seed=1, n_proposers=1, n_acceptors=3, n_ticks=3, tick_period=10)
+    r = R.run_instance(cfg, 0)
+    assert r.flags == 0 and r.rounds == 3 and r.executes == 3
+    assert R.cmd_str(r.decided_val) == "c1.1" and r.decided_ticket == 1
+    assert r.messages == 3 * 15 and r.steps == 20 + 6
+    for a in r.acceptors:
+        assert [R.cmd_str(v) for v in a.log] == ["c1.1", "c1.2", "c1.3"] and a.t_max == 3
+
+
+def test_log_mode_tick_while_busy_is_dropped():
+    """A Tick that finds the proposer in Round1/Round2 is ignored
+    (Client.hs:196-199): ticks at 0, 2, 4, 6 commit c1.1 and c1.2 only."""
+    cfg = R.Config(seed=1, n_proposers=1, n_acceptors=3, n_ticks=4, tick_period=2)
+    r = R.run_instance(cfg, 0)
+    assert r.executes == 2 and r.rounds == 2
+    for a in r.acceptors:
+        assert [R.cmd_str(v) for v in a.log] == ["c1.1", "c1.2"]
+
+
+def test_single_tick_config_is_unchanged_by_log_fields():
+    base = R.Config(seed=9, n_proposers=2, n_acceptors=5, loss_ppm=100000, delay_max=4, skew_max=3)
+    one = R.Config(seed=9, n_proposers=2, n_acceptors=5, loss_ppm=100000, delay_max=4, skew_max=3,
+                   n_ticks=1, tick_period=7)
+    for i in range(30):
+        a, b = R.run_instance(base, i), R.run_instance(one, i)
+        assert (a.decided_val, a.rounds, a.packed_flags(), a.canon_bytes) == \
+               (b.decided_val, b.rounds, b.packed_flags(), b.canon_bytes)
+
+
+@pytest.mark.parametrize("P,N,loss,delay,ticks,period", [
+    (1, 3, 0, 1, 4, 3), (2, 5, 50000, 3, 6, 9), (3, 7, 150000, 4, 5, 20), (2, 4, 0, 6, 8, 5)])
+def test_c_oracle_matches_python_log_mode(P, N, loss, delay, ticks, period):
+    cfg = pxb.Config(seed=0x10C + P * N, n_proposers=P, n_acceptors=N, loss_ppm=loss,
+                     delay_max=delay, skew_max=2, step_cap=400, n_ticks=ticks, tick_period=period)
+    rcfg = R.Config(**{k: getattr(cfg, k) for k in R.Config.__dataclass_fields__})
+    n = 40
+    res, dig, acc, cnt = oracle_c.run_cpu(cfg, 5, n, threads=2, want_acceptors=True)
+    canon = execs = 0
+    for i in range(n):
+        r = R.run_instance(rcfg, 5 + i)
+        canon += r.canon_bytes
+        execs += r.executes
+        assert list(res[i]) == [r.decided_val, r.decided_ticket, r.rounds, r.packed_flags()]
+        assert list(dig[i]) == [r.digest(a) for a in range(N)]
+        assert [int(x) for x in acc[i, :, 3]] == [len(a.log) | (int(a.dead) << 31) for a in r.acceptors]
+    assert cnt["canon_bytes"] == canon and cnt["executes"] == execs
+
+
 # ---- C restatement == Python restatement == golden fixtures ----------------------
 @pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "cfg*.npz"))))
 def test_c_oracle_matches_golden(path):

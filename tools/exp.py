@@ -39,9 +39,11 @@ def main():
         ms, t = timeit(pxb.CONFIGS[2], 1 << 20, False, 20, 0)
         row.append("c2-noout %.4f" % ms)
         ms, t = timeit(pxb.CONFIGS[3], 1 << 22, True, 3, 0)
-        row.append("c3 %.2f ms (%.1f Minst/s)" % (ms, (1 << 22) / ms / 1e3))
+        row.append("c3 %.2f ms (%.1f Minst/s, %.1f ps/inst-step, %.1f ps/msg)" % (
+            ms, (1 << 22) / ms / 1e3, ms * 1e9 * 4 / t[12], ms * 1e9 * 4 / t[7]))
         ms, t = timeit(pxb.CONFIGS[5], 1 << 20, True, 2, 0)
-        row.append("c5 %.2f ms (%.1f Minst/s)" % (ms, (1 << 20) / ms / 1e3))
+        row.append("c5 %.2f ms (%.1f Minst/s, %.1f ps/inst-step, %.1f ps/msg)" % (
+            ms, (1 << 20) / ms / 1e3, ms * 1e9 * 3 / t[12], ms * 1e9 * 3 / t[7]))
         print("%-28s %s" % (lib, " | ".join(row)), flush=True)
 
 
