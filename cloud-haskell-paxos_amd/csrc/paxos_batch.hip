@@ -186,7 +186,11 @@ __device__ __forceinline__ uint4 philox_here(uint32_t c0, uint32_t c1, uint32_t 
   return philox(c0, c1, c2, c3, k0, k1);
 }
 
-template <int PM, int N, bool LOGM>
+// FF = fault-free schedule (no loss, delay 1, no crash windows, no fuzzing):
+// every message is due exactly one step after it is sent, so a link's due
+// count is its length (requests) or its length before this step's acceptor
+// phase (responses), and no Philox draw, due-nibble or isolation test is needed.
+template <int PM, int N, bool LOGM, bool FF>
 __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KParams kp) {
   constexpr int G = 64 / N;
   constexpr uint32_t NM = (1u << N) - 1u;     // slot-local lane mask
@@ -265,7 +269,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
     Lk.seq = pred ? k + 1u : k;
     int32_t d = 1;
     bool ok = true;
-    if (pred && faulty) {
+    if (!FF && pred && faulty) {
       const uint64_t inst = kp.first_instance + idx;
       const uint4 w = philox_here((uint32_t)inst, (uint32_t)(inst >> 32), k, (1u << 24) | dirbits | (uint32_t)a, k0, k1);
       ok = !(lossy && w.x <= loss_m1);
@@ -276,14 +280,18 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
     const bool push = pred && ok && !full;
     const bool ovf = pred && ok && full;
     if (any(ovf)) lflags |= ovf ? (uint32_t)PXB_F_QUEUE_OVERFLOW : 0u;
-    const int32_t due = max(s + d, l_last(Lk));
+    const int32_t due = FF ? s + 1 : max(s + d, l_last(Lk));
     if (push) {
       const uint32_t at = ((l_head(Lk) + len) & 7u) * 64u + (uint32_t)lane;
       ring[at] = word;
       if (ring2) ring2[at] = word2;
     }
-    Lk.dn = push ? (Lk.dn | (((uint32_t)due & 15u) << (4u * len))) : Lk.dn;
-    Lk.hl = push ? (((Lk.hl & 0x7Fu) + 1u) | ((uint32_t)due << 8)) : Lk.hl;
+    if constexpr (FF) {
+      Lk.hl = push ? Lk.hl + 1u : Lk.hl;        // no due bookkeeping: all due next step
+    } else {
+      Lk.dn = push ? (Lk.dn | (((uint32_t)due & 15u) << (4u * len))) : Lk.dn;
+      Lk.hl = push ? (((Lk.hl & 0x7Fu) + 1u) | ((uint32_t)due << 8)) : Lk.hl;
+    }
   };
   // proposer p's broadcast copy on link p -> a (sendToAllServers, Client.hs:122-123)
   auto send_req = [&](auto pc, bool has, uint32_t kind, int32_t x, uint32_t z) {
@@ -351,7 +359,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
         bool crashy = (kp.cfg & CFG_CRASHY) != 0u;
         loss_m1 = kp.loss_m1;
         uint32_t crash_m1 = kp.crash_m1;
-        if (kp.cfg & CFG_RANDOMIZE) {                  // SEMANTICS §4 (config-5 fuzz)
+        if (!FF && (kp.cfg & CFG_RANDOMIZE)) {         // SEMANTICS §4 (config-5 fuzz)
           const uint4 w = philox(ilo, ihi, 0u, 4u << 24, k0, k1);
           P = 1u + mulhi_n(w.x, kp.n_prop);
           const uint64_t lt = prob_threshold(mulhi_n(w.y, kp.loss_ppm + 1u));
@@ -379,7 +387,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
           Sx[p] = Link{0, 0, 0};
         });
         c0 = c1 = 0;
-        if (crashy) {
+        if (!FF && crashy) {
           const uint4 w = philox(ilo, ihi, 0u, (3u << 24) | (uint32_t)a, k0, k1);
           if (w.x <= crash_m1) {
             c0 = (int32_t)mulhi_n(w.y, kp.crash_start_max + 1u);
@@ -403,15 +411,20 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
     STAMP(0);
 
     const uint32_t srep = ((uint32_t)s & 15u) * 0x11111111u;
+    // FF: the responses due now are exactly those queued before this step's
+    // acceptor phase (the replies it sends are due next step)
+    uint32_t sx_due[PM];
+#pragma unroll
+    for (int p = 0; p < PM; ++p) sx_due[p] = FF ? l_len(Sx[p]) : 0u;
     // ---------------- acceptor phase: (proposer index, link seq) order -------
     // handleClientRequest, Server.hs:51-78, for every due request of lane a;
     // the first due request of every lane is handled straight-line, further
     // ones (delay > 1 bunching) in a loop.
     {
-      const bool isolated = (c0 <= s) && (s < c1);
+      const bool isolated = !FF && (c0 <= s) && (s < c1);
       static_for<0, PM>([&](auto pc) {
         constexpr int p = decltype(pc)::value;
-        uint32_t cnt = active ? l_due_count(R[p], srep) : 0u;
+        uint32_t cnt = active ? (FF ? l_len(R[p]) : l_due_count(R[p], srep)) : 0u;
         if (any(cnt > 0u)) {
           do {
             acc_take(pc, cnt > 0u, isolated);
@@ -446,7 +459,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
         }
         send_req(pc, no > 0u, o0.kind, o0.x, o0.z);
       }
-      const uint32_t cnt_p = pact ? l_due_count(Sx[p], srep) : 0u;
+      const uint32_t cnt_p = pact ? (FF ? sx_due[p] : l_due_count(Sx[p], srep)) : 0u;
       const uint64_t anyb = ballot(cnt_p > 0u);
       STAMP(2);
       if (anyb != 0ull) {
@@ -715,30 +728,36 @@ __global__ void proposer_hook_kernel(pxb_proposer_rec* st, uint32_t n_acc, const
 // ---- host side ----------------------------------------------------------------
 typedef void (*kernel_fn)(KParams);
 
-template <int PM, int N, bool LOGM>
-static kernel_fn kfn() { return paxos_batch_kernel<PM, N, LOGM>; }
+template <int PM, int N, bool LOGM, bool FF>
+static kernel_fn kfn() { return paxos_batch_kernel<PM, N, LOGM, FF>; }
 
-template <int PM, bool LOGM>
+template <int PM, bool LOGM, bool FF>
 static kernel_fn pick_n(uint32_t n) {
   switch (n) {
-    case 2: return kfn<PM, 2, LOGM>();
-    case 3: return kfn<PM, 3, LOGM>();
-    case 4: return kfn<PM, 4, LOGM>();
-    case 5: return kfn<PM, 5, LOGM>();
-    case 6: return kfn<PM, 6, LOGM>();
-    case 7: return kfn<PM, 7, LOGM>();
-    case 8: return kfn<PM, 8, LOGM>();
-    case 9: return kfn<PM, 9, LOGM>();
+    case 2: return kfn<PM, 2, LOGM, FF>();
+    case 3: return kfn<PM, 3, LOGM, FF>();
+    case 4: return kfn<PM, 4, LOGM, FF>();
+    case 5: return kfn<PM, 5, LOGM, FF>();
+    case 6: return kfn<PM, 6, LOGM, FF>();
+    case 7: return kfn<PM, 7, LOGM, FF>();
+    case 8: return kfn<PM, 8, LOGM, FF>();
+    case 9: return kfn<PM, 9, LOGM, FF>();
   }
   return nullptr;
 }
 
-// single decree (one Tick per proposer) or log mode (several)
-static kernel_fn pick(uint32_t pm, uint32_t n, bool logm) {
+template <int PM>
+static kernel_fn pick_mode(uint32_t n, bool logm, bool ff) {
+  if (logm) return ff ? pick_n<PM, true, true>(n) : pick_n<PM, true, false>(n);
+  return ff ? pick_n<PM, false, true>(n) : pick_n<PM, false, false>(n);
+}
+
+// single decree (one Tick per proposer) or log mode (several); fault-free or not
+static kernel_fn pick(uint32_t pm, uint32_t n, bool logm, bool ff) {
   switch (pm) {
-    case 1: return logm ? pick_n<1, true>(n) : pick_n<1, false>(n);
-    case 2: return logm ? pick_n<2, true>(n) : pick_n<2, false>(n);
-    case 3: return logm ? pick_n<3, true>(n) : pick_n<3, false>(n);
+    case 1: return pick_mode<1>(n, logm, ff);
+    case 2: return pick_mode<2>(n, logm, ff);
+    case 3: return pick_mode<3>(n, logm, ff);
   }
   return nullptr;
 }
@@ -748,7 +767,7 @@ static thread_local int g_last_hip = 0;
 static unsigned long long* g_dbg = nullptr;
 #endif
 static std::mutex g_mu;
-static int g_occ[2][4][10][64];         // [logm][pm][n][device] blocks per CU (0 = unknown)
+static int g_occ[4][4][10][64];         // [logm*2+ff][pm][n][device] blocks per CU (0 = unknown)
 static int g_cus[64];
 
 static int hip_fail(hipError_t e) {
@@ -820,7 +839,11 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
   HIPCHK(hipGetDevice(&dev));
   if (dev < 0 || dev >= 64) return PXB_E_NODEV;
   const bool logm = cfg->n_ticks > 1;   // log mode: several Ticks per proposer
-  kernel_fn fn = pick(cfg->n_proposers, cfg->n_acceptors, logm);
+  // fault-free schedule: no message is lost, delayed past the next step or sent
+  // to an isolated acceptor (Tick skew is allowed)
+  const bool ff = !(cfg->flags & PXB_CFG_RANDOMIZE) && cfg->loss_ppm == 0 && cfg->delay_max == 1 &&
+                  cfg->crash_ppm == 0;
+  kernel_fn fn = pick(cfg->n_proposers, cfg->n_acceptors, logm, ff);
   if (!fn) return PXB_E_INVAL;
   const hipStream_t st = (hipStream_t)stream;
   int occ, cus;
@@ -831,7 +854,7 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
       HIPCHK(hipGetDeviceProperties(&prop, dev));
       g_cus[dev] = prop.multiProcessorCount;
     }
-    int& o = g_occ[logm ? 1 : 0][cfg->n_proposers][cfg->n_acceptors][dev];
+    int& o = g_occ[(logm ? 2 : 0) + (ff ? 1 : 0)][cfg->n_proposers][cfg->n_acceptors][dev];
     if (!o) {
       int nb = 0;
       HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)fn, BLOCK, 0));

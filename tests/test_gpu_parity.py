@@ -52,6 +52,17 @@ def test_topology_sweep(gpu_lib, P, N):
     _cmp(cfg, 1000, 3001)
 
 
+@pytest.mark.parametrize("P", [1, 2, 3])
+@pytest.mark.parametrize("N", [2, 3, 5, 8, 9])
+def test_fault_free_topology_sweep(gpu_lib, P, N):
+    """Fault-free schedules run the FF kernels (due counts from queue lengths,
+    no Philox): duelling proposers with Tick skew, single decree and log mode."""
+    for ticks in (1, 5):
+        cfg = pxb.Config(seed=0xFF00 + 16 * P + N, n_proposers=P, n_acceptors=N, skew_max=2,
+                         step_cap=600, n_ticks=ticks, tick_period=7)
+        _cmp(cfg, 77, 2501)
+
+
 @pytest.mark.parametrize("kw", [
     dict(loss_ppm=0, delay_max=15),                 # max delay, FIFO max() rule
     dict(loss_ppm=1000000),                          # everything lost
