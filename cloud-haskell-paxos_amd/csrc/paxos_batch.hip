@@ -1,31 +1,9 @@
-// paxos_batch.hip — gfx950 batched single-decree ticket-Paxos engine + C ABI.
+// paxos_batch.hip — host side of the gfx950 batched ticket-Paxos engine: the
+// C ABI (include/paxos_batch.h), launch configuration, dispatch over the
+// kernel instantiations, and the single-handler hook kernels.
 //
-// Replaces the reference's per-message actors (Server.hs:44-89 acceptor loop,
-// Client.hs:85-111 proposer loop, spawned by Main.hs:41-46) with one GPU wave
-// per group of independent instances:
-//
-//   * lane = (instance slot g, acceptor a): G = 64 / N instance slots per wave,
-//     lanes g*N .. g*N+N-1 hold the N acceptors of one instance (SoA in VGPRs).
-//     The kernel is VALU-issue bound (throughput saturates at 2-3 waves per
-//     SIMD), so state stays unpacked and every hot-path instruction counts.
-//   * each acceptor lane owns its directed links: the request queue from every
-//     proposer p (p -> a) and the response queue to every proposer (a -> p),
-//     PXB_QUEUE_DEPTH deep, as lane-interleaved LDS rings (bank-conflict free)
-//     with the due steps nibble-packed in one register per link.
-//   * the P proposers of an instance are replicated in all N lanes of its
-//     slot.  Responses are folded in canonical (acceptor, link seq) order:
-//     quorum counting with __ballot + popcount, the majority acceptor from a
-//     prefix popcount, MostRecent (Common.hs:61-65) from a slot max-reduction;
-//     a serial ds_bpermute fold handles the rare slot with 2+ due responses on
-//     one link.  Each lane enqueues its own copy of a broadcast on its own
-//     link (Philox loss/delay per link, in parallel).
-//   * waves are persistent: when a slot's instance quiesces (or hits
-//     step_cap) the slot writes its 16-B result + 4-B/acceptor digests and
-//     refills from the wave's contiguous instance range.
-//   * run totals: slot leaders count finished instances in packed 16-bit
-//     per-lane counters, reduced once per wave when the wave exits.
-//
-// Semantics: docs/SEMANTICS.md; checked bit-exact against oracle/.
+// The batch kernel itself is paxos_kernel.h (design notes there and in
+// DESIGN.md); its instantiations are compiled by paxos_inst.hip.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -34,659 +12,22 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
-#include <type_traits>
 
 #include "../../include/paxos_batch.h"
-#include "paxos_device.h"
+#include "paxos_kernel.h"
 
 namespace pxb {
 
-constexpr int QD = PXB_QUEUE_DEPTH;   // 8: ring slots per directed link
-constexpr int LT = PXB_LOG_TRACK;
-static_assert(QD == 8, "due-nibble word and ring masks assume 8 slots");
-static_assert(PXB_MAX_STEP_CAP <= 8192, "14-bit packed tickets / steps");
-#ifndef PXB_WPB
-#define PXB_WPB 1
-#endif
-constexpr int WPB = PXB_WPB;          // waves per block (LDS is carved per wave)
-constexpr int BLOCK = 64 * WPB;
-#ifndef PXB_OCC_P1
-#define PXB_OCC_P1 4
-#endif
-#ifndef PXB_OCC_P2
-#define PXB_OCC_P2 3
-#endif
-#ifndef PXB_OCC_P3
-#define PXB_OCC_P3 2
-#endif
-
-// kp.cfg bit layout
-constexpr uint32_t CFG_RANDOMIZE = 1u << 0;
-constexpr uint32_t CFG_LOSSY = 1u << 1;     // loss threshold > 0
-constexpr uint32_t CFG_CRASHY = 1u << 2;    // crash threshold > 0
-
-struct KParams {
-  uint64_t first_instance;
-  uint32_t n_instances;               // this launch (host chunks larger batches)
-  uint32_t k0, k1;                    // Philox key = seed
-  uint32_t cfg;                       // CFG_*
-  uint32_t n_prop, delay_max;
-  uint32_t loss_m1, crash_m1;         // thr-1 (valid when LOSSY / CRASHY)
-  uint32_t loss_ppm, crash_ppm;       // maxima for RANDOMIZE
-  uint32_t crash_len_max, crash_start_max, skew_max, step_cap;
-  uint32_t n_ticks, tick_period;      // log mode (LOGM kernels): Ticks per proposer, spacing
-  uint4* out;                         // pxb_result records (nullable)
-  uint32_t* dig;
-  uint4* acc;
-  unsigned long long* totals;
-  unsigned long long* dbg;            // diagnostic builds only (PXB_STAMPS)
-};
-
-__host__ __device__ inline uint64_t prob_threshold(uint32_t ppm) {
-  return ((((uint64_t)ppm) << 32) + 999999ull) / 1000000ull;
-}
-
-// wave ballot straight from the lane predicate (HIP's __ballot(int) adds a
-// bool -> int -> compare round trip per call)
-__device__ __forceinline__ uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
-__device__ __forceinline__ bool any(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0ull; }
-
-// compile-time loop: every per-proposer register index is a constant
-template <int I, int E, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (I < E) {
-    f(std::integral_constant<int, I>{});
-    static_for<I + 1, E>(f);
-  }
-}
-
-// ---- diagnostic section stamps (separate build: -DPXB_STAMPS; never timed) --
-#ifdef PXB_STAMPS
-#define STAMP_DECL uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; uint64_t st_prev = __builtin_amdgcn_s_memtime();
-#define STAMP(i)                                                  \
-  do {                                                            \
-    __builtin_amdgcn_sched_barrier(0);                            \
-    const uint64_t st_now = __builtin_amdgcn_s_memtime();         \
-    __builtin_amdgcn_sched_barrier(0);                            \
-    st_acc[i] += st_now - st_prev;                                \
-    st_prev = st_now;                                             \
-  } while (0)
-#define STAMP_FLUSH(ptr)                                          \
-  if (lane == 0 && (ptr)) {                                       \
-    for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&(ptr)[i_], (unsigned long long)st_acc[i_]); \
-  }
-#else
-#define STAMP_DECL
-#define STAMP(i) do {} while (0)
-#define STAMP_FLUSH(ptr)
-#endif
-
-// ---- one directed link = LDS ring (payload) + 3 registers ------------------
-// Every message is one 32-bit word:
-//   request   x[13:0] | val[15:14] | kind[17:16]
-//   response  x[13:0] | y[27:14]   | val[29:28] | kind[31:30]
-// The due steps (mod 16) of the queued messages sit in one register as a
-// nibble shift-queue, so "how many are due now" needs no LDS access.
-struct Link {
-  uint32_t dn;    // due&15 of entry i in bits [4i+3:4i], entry 0 = head
-  uint32_t hl;    // len[3:0] | head[6:4] | 0[7] | last_due[31:8]
-  uint32_t seq;   // sends attempted on this link (Philox counter word 2)
-};
-__device__ __forceinline__ uint32_t l_len(const Link& L) { return L.hl & 15u; }
-__device__ __forceinline__ uint32_t l_head(const Link& L) { return (L.hl >> 4) & 7u; }
-__device__ __forceinline__ int32_t l_last(const Link& L) { return (int32_t)(L.hl >> 8); }
-// find-first-set-bit with the hardware's "none" value (v_ffbl_b32: ~0u for 0)
-__device__ __forceinline__ uint32_t ffbl(uint32_t x) { return x ? (uint32_t)__builtin_ctz(x) : ~0u; }
-// number of entries at the head that are due at step s (due == s <=> nibble ==
-// s&15, because every queued due lies in [s, s+15]); srep = (s&15) * 0x11111111
-__device__ __forceinline__ uint32_t l_due_count(const Link& L, uint32_t srep) {
-  return min(ffbl(L.dn ^ srep) >> 2, l_len(L));
-}
-// pop the head when `p`: len - 1, head + 1 (mod 8: the carry into bit 7 is cleared)
-__device__ __forceinline__ void l_pop_if(Link& L, bool p) {
-  L.dn = p ? (L.dn >> 4) : L.dn;
-  L.hl = p ? ((L.hl + 15u) & ~0x80u) : L.hl;
-}
-
-// Log mode (several Ticks per proposer, SEMANTICS §9) carries full commands
-// "c<id>.<t>" (16 bits: id << 14 | t) instead of the single-decree clientId:
-// a Round1OK then needs a second word, kept in a parallel ring.
-template <int PM, bool LOGM> struct Ring2 { uint32_t w[PM][QD][64]; };
-template <int PM> struct Ring2<PM, false> { uint32_t w[1][1][1]; };
-
-template <int PM, int N, bool LOGM>
-struct Lds {
-  static constexpr int G = 64 / N;
-  using clog_t = std::conditional_t<LOGM, unsigned long long, uint32_t>;
-  uint32_t rq[PM][QD][64];       // links p -> a   (lane-interleaved: conflict-free)
-  uint32_t sq[PM][QD][64];       // links a -> p
-  clog_t clog[G][LT + 1];        // per-slot canonical log (+1 pad: rows on distinct banks);
-                                 // entries are (epoch << CB | command), epoch = instance tag
-  Ring2<PM, LOGM> sq2;           // links a -> p, command word (log mode)
-};
-
-// command word -> the result encoding (clientId << 24) | t of "c<id>.<t>"
-template <bool LOGM>
-__device__ __forceinline__ uint32_t code32(uint32_t v) {
-  if constexpr (LOGM) return v ? (((v >> 14) << 24) | (v & 0x3FFFu)) : 0u;
-  else return v ? ((v << 24) | 1u) : 0u;
-}
-
-// occupancy target (waves per SIMD) by proposer count: bounds the VGPR budget
-template <int PM> struct Occ { static constexpr int waves = PXB_OCC_P1; };
-template <> struct Occ<2> { static constexpr int waves = PXB_OCC_P2; };
-template <> struct Occ<3> { static constexpr int waves = PXB_OCC_P3; };
-
-// Philox with its inputs made opaque, so the compiler cannot hoist the
-// per-instance half of the rounds (quarter-rate multiplies) out of the rare
-// fault branch into every step.
-__device__ __forceinline__ uint4 philox_here(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
-                                             uint32_t k0, uint32_t k1) {
-  asm volatile("" : "+v"(c0), "+v"(c1), "+s"(k0), "+s"(k1));
-  return philox(c0, c1, c2, c3, k0, k1);
-}
-
-// FF = fault-free schedule (no loss, delay 1, no crash windows, no fuzzing):
-// every message is due exactly one step after it is sent, so a link's due
-// count is its length (requests) or its length before this step's acceptor
-// phase (responses), and no Philox draw, due-nibble or isolation test is needed.
-template <int PM, int N, bool LOGM, bool FF>
-__global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KParams kp) {
-  constexpr int G = 64 / N;
-  constexpr uint32_t NM = (1u << N) - 1u;     // slot-local lane mask
-  constexpr uint32_t ENONE = 16u;             // "no event" acceptor index (N <= 9 < 16)
-  // command field of a request word: single decree = clientId (2 bits, t = 1),
-  // log mode = id << 14 | t (16 bits); the kind sits above it
-  constexpr uint32_t ZM = LOGM ? 0xFFFFu : 3u, KSH = LOGM ? 30u : 16u;
-  using clog_t = typename Lds<PM, N, LOGM>::clog_t;
-  constexpr uint32_t CB = LOGM ? 32u : 2u;    // epoch shift of a canonical-log entry
-  __shared__ Lds<PM, N, LOGM> s_lds[WPB];
-
-  const int lane = threadIdx.x & 63;
-  const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  Lds<PM, N, LOGM>& L = s_lds[wib];
-  const int g = lane / N;
-  const int a = lane - g * N;
-  const bool used = g < G;
-  const int base = g * N;
-  const uint32_t ltm = (1u << a) - 1u;        // slot-local lanes below me
-  clog_t* clog = &L.clog[used ? g : 0][0];
-  for (int k = lane; k < G * (LT + 1); k += 64) (&L.clog[0][0])[k] = 0u;   // epoch 0 = empty
-  // a ballot restricted to my slot, as an N-bit mask indexed by acceptor
-  auto slot = [&](uint64_t b) -> uint32_t { return (uint32_t)(b >> base) & NM; };   // unused lanes never act
-
-  const uint32_t wave = blockIdx.x * WPB + wib;
-  const uint32_t nwaves = gridDim.x * WPB;
-  const uint32_t n = kp.n_instances;
-  uint32_t next = (uint32_t)((uint64_t)n * wave / nwaves);
-  const uint32_t first_idx = next;
-  const uint32_t end = (uint32_t)((uint64_t)n * (wave + 1) / nwaves);
-  const uint32_t k0 = kp.k0, k1 = kp.k1;
-
-  // ---- slot state (replicated in the slot's lanes unless marked "lane") ----
-  bool active = false;
-  uint32_t P = 0, dmax = 1;
-  bool faulty = false, lossy = false, tovf = false;
-  int32_t last_tick = 0;
-  int32_t s = 0;                          // current step
-  uint32_t idx = 0;                       // local instance index
-  uint32_t loss_m1 = 0;
-  uint32_t rounds = 0, dval = 0;          // dval: decided clientId (0 = none)
-  int32_t dtick = 0;
-  int32_t c0 = 0, c1 = 0;                 // lane: isolation window of acceptor a
-  AccState A{0, 0, 0, false};             // lane: acceptor a (ServerState)
-  uint32_t log_len = 0, lflags = 0, digest = 0;   // lane
-  uint32_t canon = 0;                     // lane: canonical bytes of the current instance
-  PropState S[PM];                        // replicated proposers (ClientState)
-  int32_t skew[PM];
-  int32_t ntick[PM];                      // log mode: step of proposer p's next Tick
-  uint32_t tleft[PM];                     // log mode: Ticks still to come
-  uint32_t execs = 0, execs_acc = 0;      // Execute broadcasts (commands committed)
-  Link R[PM], Sx[PM];                     // lane: links p -> a, a -> p
-  uint32_t msgs_acc = 0;                  // lane totals across instances
-  uint64_t canon_acc = 0;
-  // slot-leader run totals, two 16-bit counts per register (the host sizes
-  // launches so no slot finishes 65536 instances):
-  //   ca = instances | undecided<<16, cb = stuck | panic<<16,
-  //   cc = divergence | step_cap<<16, cd = queue_ovf | ticket_ovf<<16, ce = log_trunc
-  uint32_t ca = 0, cb = 0, cc = 0, cd = 0, ce = 0, rounds_acc = 0, steps_acc = 0;
-#pragma unroll
-  for (int p = 0; p < PM; ++p) {
-    S[p] = PropState{0, 0, 0, IDLE, 0, 0, 0, 0, 0u};
-    skew[p] = 0;
-    ntick[p] = 0;
-    tleft[p] = 0;
-    R[p] = Link{0, 0, 0};
-    Sx[p] = Link{0, 0, 0};
-  }
-
-  // common link send, predicated on `pred` (docs/SEMANTICS.md §5): Philox
-  // loss/delay, FIFO due, bounded ring (overflow -> flag, message dropped)
-  auto link_send = [&](Link& Lk, uint32_t* ring, uint32_t* ring2, uint32_t dirbits, uint32_t word,
-                       uint32_t word2, bool pred) {
-    msgs_acc += pred ? 1u : 0u;
-    const uint32_t k = Lk.seq;
-    Lk.seq = pred ? k + 1u : k;
-    int32_t d = 1;
-    bool ok = true;
-    if (!FF && pred && faulty) {
-      const uint64_t inst = kp.first_instance + idx;
-      const uint4 w = philox_here((uint32_t)inst, (uint32_t)(inst >> 32), k, (1u << 24) | dirbits | (uint32_t)a, k0, k1);
-      ok = !(lossy && w.x <= loss_m1);
-      d = 1 + (int32_t)mulhi_n(w.y, dmax);
-    }
-    const uint32_t len = l_len(Lk);
-    const bool full = len >= (uint32_t)QD;
-    const bool push = pred && ok && !full;
-    const bool ovf = pred && ok && full;
-    if (any(ovf)) lflags |= ovf ? (uint32_t)PXB_F_QUEUE_OVERFLOW : 0u;
-    const int32_t due = FF ? s + 1 : max(s + d, l_last(Lk));
-    if (push) {
-      const uint32_t at = ((l_head(Lk) + len) & 7u) * 64u + (uint32_t)lane;
-      ring[at] = word;
-      if (ring2) ring2[at] = word2;
-    }
-    if constexpr (FF) {
-      Lk.hl = push ? Lk.hl + 1u : Lk.hl;        // no due bookkeeping: all due next step
-    } else {
-      Lk.dn = push ? (Lk.dn | (((uint32_t)due & 15u) << (4u * len))) : Lk.dn;
-      Lk.hl = push ? (((Lk.hl & 0x7Fu) + 1u) | ((uint32_t)due << 8)) : Lk.hl;
-    }
-  };
-  // proposer p's broadcast copy on link p -> a (sendToAllServers, Client.hs:122-123)
-  auto send_req = [&](auto pc, bool has, uint32_t kind, int32_t x, uint32_t z) {
-    constexpr int p = decltype(pc)::value;
-    rounds += (has && kind == ASK) ? 1u : 0u;
-    const bool ex = has && kind == EXECUTE;
-    if (any(ex)) {                      // a slot committed (Client.hs:178)
-      execs += ex ? 1u : 0u;
-      const bool first_exec = ex && dval == 0u;   // the decided value
-      dval = first_exec ? S[p].r2_v : dval;
-      dtick = first_exec ? x : dtick;
-    }
-    link_send(R[p], &L.rq[p][0][0], nullptr, (uint32_t)p << 8, (uint32_t)x | (z << 14) | (kind << KSH), 0u, has);
-  };
-  // one request from the head of link p -> a, predicated on `due`:
-  // handleClientRequest, Server.hs:51-78 (dead / isolated acceptors discard it)
-  auto acc_take = [&](auto pc, bool due, bool isolated) {
-    constexpr int p = decltype(pc)::value;
-    const uint32_t w = L.rq[p][l_head(R[p])][lane];
-    l_pop_if(R[p], due);
-    const uint32_t kind = (w >> KSH) & 3u;
-    const bool live = due && !A.dead && !isolated;
-    const uint32_t rb = 8u + ((kind & 1u) << 2);       // payload: Propose 12, Ask / Execute 8
-    canon += live ? 2u * rb + 32u : (due ? rb : 0u);    // discarded: written, not read
-    int32_t rx, ry;
-    uint32_t rz, ev;
-    const uint32_t rk = acceptor_step(A, live, kind, (int32_t)(w & 0x3FFFu), (w >> 14) & ZM, rx, ry, rz, ev);
-    if (any(ev != 0u)) {
-      if (ev != 0u) {
-        digest = fnv_u32(digest, code32<LOGM>(ev));
-        if (log_len < (uint32_t)LT) {
-          // two acceptors of this instance executed different commands at
-          // the same position iff the max already holds this epoch with
-          // another command (order-independent, SEMANTICS §7)
-          const clog_t tag = (clog_t)(idx - first_idx + 1u);
-          const clog_t old = atomicMax(&clog[log_len], (tag << CB) | (clog_t)ev);
-          if ((old >> CB) == tag && (uint32_t)(old & (((clog_t)1 << CB) - 1u)) != ev) lflags |= PXB_F_LOG_DIVERGENCE;
-        } else {
-          lflags |= PXB_F_LOG_TRUNC;
-        }
-        log_len++;
-      }
-    }
-    // tickets are < 2^14 (SEMANTICS §6), so the fields need no masking
-    // (log mode: the clientId field says Just / Nothing, the full command
-    // travels in the second ring)
-    link_send(Sx[p], &L.sq[p][0][0], LOGM ? &L.sq2.w[p][0][0] : nullptr, (1u << 16) | ((uint32_t)p << 8),
-              (uint32_t)rx | ((uint32_t)ry << 14) | ((LOGM ? (rz >> 14) : rz) << 28) | (rk << 30), rz,
-              rk != NONE);
-  };
-
-  STAMP_DECL
-  for (;;) {
-    // ---------------- refill free slots from this wave's range -------------
-    const uint64_t freeb = ballot(used && !active && a == 0);
-    if (freeb != 0ull && next < end) {
-      const uint32_t cand = next + (uint32_t)__popcll(freeb & ((1ull << base) - 1ull));
-      if (used && !active && cand < end) {
-        idx = cand;
-        const uint64_t inst = kp.first_instance + cand;
-        const uint32_t ilo = (uint32_t)inst, ihi = (uint32_t)(inst >> 32);
-        P = kp.n_prop;
-        dmax = kp.delay_max;
-        lossy = (kp.cfg & CFG_LOSSY) != 0u;
-        bool crashy = (kp.cfg & CFG_CRASHY) != 0u;
-        loss_m1 = kp.loss_m1;
-        uint32_t crash_m1 = kp.crash_m1;
-        if (!FF && (kp.cfg & CFG_RANDOMIZE)) {         // SEMANTICS §4 (config-5 fuzz)
-          const uint4 w = philox(ilo, ihi, 0u, 4u << 24, k0, k1);
-          P = 1u + mulhi_n(w.x, kp.n_prop);
-          const uint64_t lt = prob_threshold(mulhi_n(w.y, kp.loss_ppm + 1u));
-          dmax = 1u + mulhi_n(w.z, kp.delay_max);
-          const uint64_t ct = prob_threshold(mulhi_n(w.w, kp.crash_ppm + 1u));
-          lossy = lt != 0ull;
-          loss_m1 = (uint32_t)(lt - 1ull);
-          crashy = ct != 0ull;
-          crash_m1 = (uint32_t)(ct - 1ull);
-        }
-        uint4 wsk = make_uint4(0, 0, 0, 0);
-        if (kp.skew_max > 0u) wsk = philox(ilo, ihi, 0u, 2u << 24, k0, k1);
-        last_tick = 0;
-        static_for<0, PM>([&](auto pc) {
-          constexpr int p = decltype(pc)::value;
-          const uint32_t wp = (p == 0) ? wsk.x : (p == 1) ? wsk.y : wsk.z;
-          skew[p] = (kp.skew_max > 0u) ? (int32_t)mulhi_n(wp, kp.skew_max + 1u) : 0;
-          ntick[p] = skew[p];
-          tleft[p] = kp.n_ticks;
-          // the last Tick: skew + (n_ticks - 1) * period (single decree: skew)
-          if ((uint32_t)p < P)
-            last_tick = max(last_tick, skew[p] + (LOGM ? (int32_t)((kp.n_ticks - 1u) * kp.tick_period) : 0));
-          S[p] = PropState{0, 0, 0, IDLE, 0, 0, 0, 0, 0u};
-          R[p] = Link{0, 0, 0};
-          Sx[p] = Link{0, 0, 0};
-        });
-        c0 = c1 = 0;
-        if (!FF && crashy) {
-          const uint4 w = philox(ilo, ihi, 0u, (3u << 24) | (uint32_t)a, k0, k1);
-          if (w.x <= crash_m1) {
-            c0 = (int32_t)mulhi_n(w.y, kp.crash_start_max + 1u);
-            c1 = c0 + 1 + (int32_t)mulhi_n(w.z, kp.crash_len_max);
-          }
-        }
-        faulty = lossy || dmax > 1u;
-        tovf = false;
-        A = AccState{0, 0, 0, false};
-        log_len = lflags = 0;
-        canon = 0;
-        digest = 0x811C9DC5u;
-        rounds = dval = execs = 0;
-        dtick = 0;
-        s = 0;
-        active = true;
-      }
-      next = min(next + (uint32_t)__popcll(freeb), end);
-    }
-    if (!any(active)) break;
-    STAMP(0);
-
-    const uint32_t srep = ((uint32_t)s & 15u) * 0x11111111u;
-    // FF: the responses due now are exactly those queued before this step's
-    // acceptor phase (the replies it sends are due next step)
-    uint32_t sx_due[PM];
-#pragma unroll
-    for (int p = 0; p < PM; ++p) sx_due[p] = FF ? l_len(Sx[p]) : 0u;
-    // ---------------- acceptor phase: (proposer index, link seq) order -------
-    // handleClientRequest, Server.hs:51-78, for every due request of lane a;
-    // the first due request of every lane is handled straight-line, further
-    // ones (delay > 1 bunching) in a loop.
-    {
-      const bool isolated = !FF && (c0 <= s) && (s < c1);
-      static_for<0, PM>([&](auto pc) {
-        constexpr int p = decltype(pc)::value;
-        uint32_t cnt = active ? (FF ? l_len(R[p]) : l_due_count(R[p], srep)) : 0u;
-        if (any(cnt > 0u)) {
-          do {
-            acc_take(pc, cnt > 0u, isolated);
-            cnt = (cnt > 0u) ? cnt - 1u : 0u;
-          } while (any(cnt > 0u));
-        }
-      });
-    }
-    STAMP(1);
-
-    // ---------------- proposer phase: Tick, then (acceptor, link seq) order --
-    static_for<0, PM>([&](auto pc) {
-      constexpr int p = decltype(pc)::value;
-      const bool pact = active && (uint32_t)p < P;
-      bool stepped = false;
-      // the ticker (Client.hs:96-100): one Tick at skew_p (single decree), or
-      // n_ticks Ticks tick_period steps apart (log mode)
-      const bool tick = LOGM ? (pact && tleft[p] != 0u && s == ntick[p]) : (pact && s == skew[p]);
-      if (any(tick)) {                          // handleTick, Client.hs:196-207
-        Req o0{NONE, 0, 0};
-        uint32_t no = 0;
-        if (tick) {
-          // command "c<id>.<t>" with t the new ticket (Client.hs:200-203);
-          // single decree: t = 1, carried as the clientId alone
-          const uint32_t cmd = LOGM ? (((uint32_t)(p + 1) << 14) | (uint32_t)(S[p].ticket + 1)) : (uint32_t)(p + 1);
-          no = proposer_tick(S[p], cmd, o0);
-          stepped = true;
-          if (LOGM) {
-            ntick[p] += (int32_t)kp.tick_period;
-            tleft[p] -= 1u;
-          }
-        }
-        send_req(pc, no > 0u, o0.kind, o0.x, o0.z);
-      }
-      const uint32_t cnt_p = pact ? (FF ? sx_due[p] : l_due_count(Sx[p], srep)) : 0u;
-      const uint64_t anyb = ballot(cnt_p > 0u);
-      STAMP(2);
-      if (anyb != 0ull) {
-        const uint32_t mine_slot = slot(anyb);
-        stepped = stepped || mine_slot != 0u;
-        const bool slot_serial = slot(ballot(cnt_p > 1u)) != 0u;
-        // ---- fast path: every link a -> p of the slot has <= 1 due response.
-        // The serial fold of Client.hs:125-189 over acceptors 0..N-1 is done in
-        // rounds, one per state-changing event (majority or NACK):
-        // acks = __ballot + popcount, the majority acceptor = the lane whose
-        // prefix popcount hits the quorum, MostRecent (Common.hs:61-65) = a
-        // slot max-reduction of (t_store, -lane) over the counted acks.  After
-        // an event only a NACK (not Idle) or a stale Round2Success (in Round2)
-        // can still act: a fresh Round1OK for the new ticket cannot exist yet.
-        // Every round is a select network (no divergent branches).
-        const bool fast = pact && !slot_serial && mine_slot != 0u;
-        if (any(fast)) {
-          const bool has = fast && cnt_p == 1u;
-          const uint32_t w = L.sq[p][l_head(Sx[p])][lane];
-          const uint32_t w2 = LOGM ? L.sq2.w[p][l_head(Sx[p])][lane] : 0u;
-          l_pop_if(Sx[p], has);
-          const uint32_t kind = has ? (w >> 30) : 3u;       // 3: no response
-          const int32_t x = (int32_t)(w & 0x3FFFu);
-          const int32_t y = (int32_t)((w >> 14) & 0x3FFFu);
-          const uint32_t z = has ? (LOGM ? w2 : ((w >> 28) & 3u)) : 0u;
-          canon += has ? 2u * (16u >> kind) : 0u;
-          uint32_t rem = slot(ballot(has));                 // unprocessed responses
-          const uint32_t havem = slot(ballot(kind == HAVE));
-          const uint32_t r2sm = slot(ballot(kind == R2S));
-          bool go = fast;
-          do {
-            PropState& Sp = S[p];
-            const uint32_t rs = Sp.rs;
-            const int32_t T = Sp.ticket;
-            const bool mine = go && ((rem >> a) & 1u) != 0u;
-            const bool is_ack = mine && ((rs == ROUND1 && kind == R1OK && x == T) ||
-                                         (rs == ROUND2 && kind == R2S));
-            const bool is_ab = mine && rs != IDLE && kind == HAVE && x >= T;
-            const uint32_t ackm = slot(ballot(is_ack));
-            const uint32_t abm = slot(ballot(is_ab));
-            const uint32_t need = (uint32_t)(N >> 1) + 1u - Sp.acks;
-            const bool is_maj = is_ack && (uint32_t)__popc(ackm & ltm) + 1u == need;
-            const uint32_t majm = slot(ballot(is_maj));
-            const uint32_t e_ab = min(ffbl(abm), ENONE);
-            const uint32_t e_mj = min(ffbl(majm), ENONE);
-            const bool mj = e_mj < e_ab;                    // majority before any NACK
-            const uint32_t e = min(e_ab, e_mj);
-            // acks counted before the event (and the majority ack itself)
-            const uint32_t counted = ackm & ((1u << (e + (mj ? 1u : 0u))) - 1u);
-            // MostRecent over the counted Round1OKs that carry a proposal
-            const bool elig = rs == ROUND1 && ((counted >> a) & 1u) != 0u && z != 0u;
-            const uint32_t zb = slot(ballot(elig));
-            uint32_t key = elig ? (((uint32_t)y << 5) | (31u - (uint32_t)a)) : 0u;
-            uint32_t bz = 0;
-            if (any(zb != 0u)) {              // some slot saw a stored proposal
-              if (any(__popc(zb) > 1)) {
-#pragma unroll
-                for (int off = 1; off < N; off <<= 1) {
-                  const uint32_t o = (uint32_t)__shfl((int)key, lane + off);
-                  if (a + off < N) key = max(key, o);
-                }
-              }
-              const int src = zb ? ((__popc(zb) > 1) ? base : base + __builtin_ctz(zb)) : lane;
-              key = (uint32_t)__shfl((int)key, src);
-              bz = (uint32_t)__shfl((int)z, zb ? base + 31 - (int)(key & 31u) : lane);
-            }
-            int32_t u = 0;
-            if (any(abm != 0u)) u = __shfl(x, abm ? base + (int)e_ab : lane);
-            // ---- the state transition of this round (Client.hs:128-189) ----
-            int32_t mt = Sp.mr_t;
-            uint32_t mv = Sp.mr_v;
-            const bool take = zb != 0u && (mv == 0u || (int32_t)(key >> 5) > mt);
-            mt = take ? (int32_t)(key >> 5) : mt;
-            mv = take ? bz : mv;
-            const bool ev = go && e != ENONE;
-            const bool r1maj = go && mj && rs == ROUND1;    // Client.hs:157-170
-            const bool r2maj = go && mj && rs == ROUND2;    // Client.hs:177-189
-            const bool nack = ev && !mj;                    // Client.hs:130-140
-            const bool restart = r2maj && Sp.pending;       // Client.hs:179-185
-            const bool idle = r2maj && !Sp.pending;         // Client.hs:186-189
-            const uint32_t r2v = (mv == 0u) ? Sp.cmd : mv;
-            const int32_t tn = nack ? u + 1 : T + 1;
-            // outputs: o0 (Propose / Execute / AskForTicket), o1 (AskForTicket on restart)
-            const uint32_t k0o = r1maj ? PROPOSE : (r2maj ? EXECUTE : ASK);
-            const int32_t x0o = nack ? tn : T;
-            const uint32_t z0o = r1maj ? r2v : 0u;
-            Sp.r2_v = r1maj ? r2v : Sp.r2_v;
-            Sp.pending = r1maj ? (mv != 0u) : Sp.pending;
-            Sp.ticket = (nack || restart) ? tn : T;
-            Sp.cmd = idle ? 0u : Sp.cmd;
-            Sp.acks = go ? (ev ? 0u : Sp.acks + (uint32_t)__popc(counted)) : Sp.acks;
-            Sp.rs = r1maj ? ROUND2 : ((nack || restart) ? ROUND1 : (idle ? IDLE : rs));
-            const bool keep_mr = go && !ev && rs == ROUND1;
-            Sp.mr_t = keep_mr ? mt : (ev ? 0 : Sp.mr_t);
-            Sp.mr_v = keep_mr ? mv : (ev ? 0u : Sp.mr_v);
-            rem = ev ? rem & ~((2u << e) - 1u) : 0u;
-            go = ev && Sp.rs != IDLE && (rem & (havem | (Sp.rs == ROUND2 ? r2sm : 0u))) != 0u;
-            if (any(ev)) send_req(pc, ev, k0o, x0o, z0o);
-            if (any(restart)) send_req(pc, restart, ASK, tn, 0u);
-          } while (any(go));
-        }
-        STAMP(3);
-        // ---- general path (a link holds >= 2 due responses): serial fold in
-        // canonical order; every lane of the slot reads the head of lane aa's
-        // link (ds_bpermute) and applies handleServerResponse; lane aa pops it.
-        const uint32_t cnt_s = slot_serial ? cnt_p : 0u;
-        if (any(cnt_s > 0u)) {
-#pragma unroll 1
-          for (int aa = 0; aa < N; ++aa) {
-            uint32_t ca_ = (uint32_t)__shfl((int)cnt_s, base + aa);
-            while (any(ca_ > 0u)) {
-              const bool take = ca_ > 0u;
-              const uint32_t mine = L.sq[p][l_head(Sx[p])][lane];
-              const uint32_t w = (uint32_t)__shfl((int)mine, base + aa);
-              uint32_t z = (w >> 28) & 3u;
-              if (LOGM) z = (uint32_t)__shfl((int)L.sq2.w[p][l_head(Sx[p])][lane], base + aa);
-              Req o0{NONE, 0, 0}, o1{NONE, 0, 0};
-              uint32_t no = 0;
-              if (take) {
-                const uint32_t kind = w >> 30;
-                no = proposer_step(S[p], (uint32_t)N, kind, (int32_t)(w & 0x3FFFu),
-                                   (int32_t)((w >> 14) & 0x3FFFu), z, o0, o1);
-                if (a == aa) canon += 2u * (16u >> kind);
-                l_pop_if(Sx[p], a == aa);
-                ca_--;
-              }
-#pragma unroll 1
-              for (uint32_t k = 0; k < 2u; ++k) {
-                const bool hs = no > k;
-                if (any(hs)) send_req(pc, hs, k ? o1.kind : o0.kind, k ? o1.x : o0.x, k ? o1.z : o0.z);
-              }
-            }
-          }
-        }
-      }
-      canon += (stepped && a == 0) ? 48u : 0u;
-      tovf = tovf || (pact && S[p].ticket >= PXB_TICKET_LIMIT);
-    });
-    STAMP(4);
-
-    // ---------------- end of step: quiescence / step cap ---------------------
-    uint32_t lens = 0;
-#pragma unroll
-    for (int p = 0; p < PM; ++p) lens |= R[p].hl | Sx[p].hl;
-    const uint64_t busyb = ballot(active && (lens & 15u) != 0u);
-    const bool quiet = active && slot(busyb) == 0u && s >= last_tick;
-    const bool cap = active && !quiet && (s + 1 >= (int32_t)kp.step_cap);
-    s += active ? 1 : 0;
-    const bool done = quiet || cap;
-    STAMP(5);
-    if (any(done)) {
-      const uint32_t pan = slot(ballot(A.dead));             // Q6: dead <=> panicked
-      const uint32_t dvg = slot(ballot((lflags & PXB_F_LOG_DIVERGENCE) != 0u));
-      const uint32_t qov = slot(ballot((lflags & PXB_F_QUEUE_OVERFLOW) != 0u));
-      const uint32_t trc = slot(ballot((lflags & PXB_F_LOG_TRUNC) != 0u));
-      if (done) {
-        uint32_t f = tovf ? (uint32_t)PXB_F_TICKET_OVERFLOW : 0u;
-        f |= pan ? (uint32_t)PXB_F_PANIC : 0u;
-        f |= dvg ? (uint32_t)PXB_F_LOG_DIVERGENCE : 0u;
-        f |= qov ? (uint32_t)PXB_F_QUEUE_OVERFLOW : 0u;
-        f |= trc ? (uint32_t)PXB_F_LOG_TRUNC : 0u;
-        f |= cap ? (uint32_t)PXB_F_STEP_CAP : 0u;
-        f |= dval ? 0u : (uint32_t)PXB_F_UNDECIDED;
-#pragma unroll
-        for (int p = 0; p < PM; ++p)
-          f |= (!cap && (uint32_t)p < P && S[p].rs != IDLE) ? (uint32_t)PXB_F_STUCK : 0u;
-        canon_acc += canon + ((a == 0) ? 20u : 4u);          // + result record + this digest
-        if (a == 0) {
-          ca += 1u + ((f & PXB_F_UNDECIDED) ? 0x10000u : 0u);
-          cb += ((f & PXB_F_STUCK) ? 1u : 0u) + ((f & PXB_F_PANIC) ? 0x10000u : 0u);
-          cc += ((f & PXB_F_LOG_DIVERGENCE) ? 1u : 0u) + ((f & PXB_F_STEP_CAP) ? 0x10000u : 0u);
-          cd += ((f & PXB_F_QUEUE_OVERFLOW) ? 1u : 0u) + ((f & PXB_F_TICKET_OVERFLOW) ? 0x10000u : 0u);
-          ce += (f & PXB_F_LOG_TRUNC) ? 1u : 0u;
-          rounds_acc += rounds;
-          steps_acc += (uint32_t)s;
-          execs_acc += execs;
-        }
-        if (a == 0 && kp.out) {
-          uint4 r;
-          r.x = code32<LOGM>(dval);
-          r.y = dval ? (uint32_t)dtick : 0u;
-          r.z = rounds;
-          r.w = (f & 0xFFu) | ((uint32_t)s << 16);
-          kp.out[idx] = r;
-        }
-        if (kp.dig) kp.dig[(uint64_t)idx * N + a] = fnv_u32(digest, log_len);
-        if (kp.acc) {
-          uint4 r;
-          r.x = (uint32_t)A.t_max;
-          r.y = (uint32_t)A.t_store;
-          r.z = code32<LOGM>(A.val);
-          r.w = log_len | ((A.dead ? 1u : 0u) << 31);
-          kp.acc[(uint64_t)idx * N + a] = r;
-        }
-        active = false;
-      }
-    }
-    STAMP(6);
-  }
-
-  STAMP(7);
-  STAMP_FLUSH(kp.dbg);
-  // ---------------- flush lane totals -----------------------------------------
-  uint32_t v[14] = {ca & 0xFFFFu, ca >> 16, cb & 0xFFFFu, cb >> 16, cc & 0xFFFFu, cc >> 16,
-                    cd & 0xFFFFu, cd >> 16, ce, rounds_acc, steps_acc, msgs_acc, execs_acc, 0u};
-  uint64_t c64 = canon_acc;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-#pragma unroll
-    for (int q = 0; q < 13; ++q) v[q] += (uint32_t)__shfl_xor((int)v[q], off);
-    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)c64, off);
-    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(c64 >> 32), off);
-    c64 += ((uint64_t)hi << 32) | lo;
-  }
-  if (lane < 14) {
-    // lane q adds counter q (one atomic per lane, no serialisation within the wave)
-    const int slot_of[14] = {PXB_C_INSTANCES, PXB_C_UNDECIDED, PXB_C_STUCK, PXB_C_PANIC, PXB_C_DIVERGENCE,
-                             PXB_C_STEP_CAP, PXB_C_QUEUE_OVERFLOW, PXB_C_TICKET_OVERFLOW, PXB_C_LOG_TRUNC,
-                             PXB_C_ROUNDS, PXB_C_STEPS, PXB_C_MESSAGES, PXB_C_EXECUTES, PXB_C_DECIDED};
-    unsigned long long val = 0;
-#pragma unroll
-    for (int q = 0; q < 13; ++q) val = (lane == q) ? (unsigned long long)v[q] : val;
-    if (lane == 13) val = (unsigned long long)v[0] - (unsigned long long)v[1];   // decided
-    if (val) atomicAdd(&kp.totals[slot_of[lane]], val);
-  }
-  if (lane == 14) atomicAdd(&kp.totals[PXB_C_CANON_BYTES], (unsigned long long)c64);
-}
+// The kernel instantiations live in paxos_inst.hip (compiled once per
+// proposer count, in parallel); declared here for the dispatch table.
+#define PXB_FOR_N(M, PM, LOGM, FF) M(PM, 2, LOGM, FF) M(PM, 3, LOGM, FF) M(PM, 4, LOGM, FF) M(PM, 5, LOGM, FF) \
+  M(PM, 6, LOGM, FF) M(PM, 7, LOGM, FF) M(PM, 8, LOGM, FF) M(PM, 9, LOGM, FF)
+#define PXB_FOR_MODES(M, PM) PXB_FOR_N(M, PM, false, false) PXB_FOR_N(M, PM, false, true) \
+  PXB_FOR_N(M, PM, true, false) PXB_FOR_N(M, PM, true, true)
+#define PXB_EXTERN(PM, N, LOGM, FF) extern template __global__ void paxos_batch_kernel<PM, N, LOGM, FF>(KParams);
+PXB_FOR_MODES(PXB_EXTERN, 1)
+PXB_FOR_MODES(PXB_EXTERN, 2)
+PXB_FOR_MODES(PXB_EXTERN, 3)
 
 // ---- single-handler hook kernels ------------------------------------------
 __global__ void acceptor_hook_kernel(pxb_acceptor_rec* st, const pxb_msg* in, pxb_msg* out, uint32_t count) {

@@ -2,7 +2,12 @@
 # bash tools/build_variant.sh <name> [-D... extra hipcc flags]  -> variants/<name>.so
 set -e
 R=$(cd $(dirname $0)/.. && pwd)
-name=$1; shift
 mkdir -p $R/variants
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-pass-failed "$@" -shared \
-  -o $R/variants/$name.so $R/cloud-haskell-paxos_amd/csrc/paxos_batch.hip $R/cloud-haskell-paxos_amd/csrc/paxos_multi.cpp -lrccl
+cd $R
+python3 -c "
+import sys, subprocess
+sys.path.insert(0, '.')
+import __graft_entry__ as g
+objs = g._hip_objects(tuple(sys.argv[2:]), tag='_' + sys.argv[1])
+subprocess.run([g.HIPCC, *g.HIPFLAGS, '-shared', '-o', 'variants/%s.so' % sys.argv[1], *objs, '-lrccl'], check=True)
+" "$@"
