@@ -115,6 +115,57 @@ def traffic_per_launch(c, n):
     return t.get("bytes_per_launch")
 
 
+def wire_bench(stream, dev, n=1 << 24, reps=5):
+    """Wire codec: Data.Binary encode / decode of n
+    ServerResponse records resident in HBM (a Round1OK-heavy mix with real
+    commands), HIP events on the launch stream.  HBM bytes per message:
+    encode 16 (pxb_msg) + 8 (offset) + record; decode record + 16 offset
+    reads + 16 (pxb_msg) + 4 (status)."""
+    import numpy as np
+    rng = np.random.default_rng(0)
+    kind = rng.choice([0, 0, 1, 2], size=n).astype(np.uint32)
+    msgs = np.zeros((n, 4), np.uint32)
+    msgs[:, 0] = kind
+    msgs[:, 1] = np.where(kind == 2, 0, rng.integers(1, 1 << 13, n))   # Round2Success has no field
+    just = (kind == 0) & (rng.random(n) < 0.5)
+    msgs[:, 2] = np.where(just, rng.integers(1, 1 << 13, n), 0)
+    msgs[:, 3] = np.where(just, (rng.integers(1, 4, n) << 24) | rng.integers(1, 1 << 13, n), 0)
+    d_m = torch.from_numpy(msgs.view(np.int32)).to(dev)
+    d_o = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    d_b = torch.zeros(n * pxb.WIRE_MAX_BYTES, dtype=torch.uint8, device=dev)
+    d_back = torch.zeros_like(d_m)
+    d_st = torch.zeros(n, dtype=torch.int32, device=dev)
+    lib = pxb.load()
+    sp = stream.cuda_stream
+    ptr = lambda t: pxb.C.c_void_p(t.data_ptr())  # noqa: E731
+
+    def enc():
+        pxb.check(lib.pxb_wire_size(ptr(d_m), n, pxb.WIRE_RESPONSE, ptr(d_o), pxb.C.c_void_p(sp)))
+        pxb.check(lib.pxb_wire_encode(ptr(d_m), n, pxb.WIRE_RESPONSE, ptr(d_o), ptr(d_b), pxb.C.c_void_p(sp)))
+
+    def dec():
+        pxb.check(lib.pxb_wire_decode(ptr(d_b), ptr(d_o), n, pxb.WIRE_RESPONSE, ptr(d_back), ptr(d_st),
+                                      pxb.C.c_void_p(sp)))
+
+    out = {"messages": n}
+    with torch.cuda.stream(stream):
+        for name, fn in (("encode", enc), ("decode", dec)):
+            fn()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(reps):
+                fn()
+            e1.record(stream)
+            stream.synchronize()
+            ms = e0.elapsed_time(e1) / reps
+            nbytes = int(d_o[-1].item())
+            moved = (24 * n + nbytes) if name == "encode" else (nbytes + 16 * n + 20 * n)
+            out[name] = {"ms": ms, "messages_per_s": n / ms * 1e3, "wire_bytes": nbytes,
+                         "hbm_GBps": moved / (ms * 1e-3) / 1e9}
+    assert torch.equal(d_back, d_m) and int(d_st.abs().sum().item()) == 0
+    return out
+
+
 def cpu_baseline(cfg, budget_s):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_c                          # CPU restatement (oracle/), baseline only
@@ -192,6 +243,7 @@ def main():
                                       "decided_per_s": ecnt["decided"] / es, "kernel_ms": ek,
                                       "canonical_GBps": canon_gbs, "canonical_frac": canon_gbs / HBM_PEAK_GBS,
                                       "counters": ecnt}
+        extra["wire_codec"] = wire_bench(stream, dev)
         # log mode: stock Main.hs topology with the ticker running (SEMANTICS §9)
         en = 1 << 20
         es, ek, ecnt = run_workload(pxb.LOG_CONFIG, en, 2, 1, 0, 1, stream, dev)

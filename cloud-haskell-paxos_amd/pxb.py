@@ -189,6 +189,13 @@ def load(path: str = LIB_PATH):
     lib.pxb_abi_version.restype = C.c_int
     lib.pxb_canonical_bytes_nofault.argtypes = [C.c_uint32]
     lib.pxb_canonical_bytes_nofault.restype = C.c_uint64
+    for name, args in (("pxb_wire_size", [vp, C.c_uint64, C.c_uint32, vp, vp]),
+                       ("pxb_wire_encode", [vp, C.c_uint64, C.c_uint32, vp, vp, vp]),
+                       ("pxb_wire_decode", [vp, vp, C.c_uint64, C.c_uint32, vp, vp, vp]),
+                       ("pxb_wire_encode_host", [vp, C.c_uint64, C.c_uint32, vp, vp, vp]),
+                       ("pxb_wire_decode_host", [vp, vp, C.c_uint64, C.c_uint32, vp, vp])):
+        getattr(lib, name).argtypes = args
+        getattr(lib, name).restype = C.c_int
     _lib = lib
     return lib
 
@@ -275,3 +282,36 @@ def proposer_handle(states, n_acceptors, msgs):
     nb = np.zeros(n, dtype=np.uint32)
     check(lib.pxb_proposer_handle(_ptr(states), n_acceptors, _ptr(msgs), _ptr(bc), _ptr(nb), n))
     return bc, nb
+
+
+# ---- wire format (include/paxos_batch.h) ------------------
+WIRE_REQUEST, WIRE_RESPONSE, WIRE_MAX_BYTES = 0, 1, 39
+WIRE_OK, WIRE_E_LENGTH, WIRE_E_TAG, WIRE_E_STRING, WIRE_E_RANGE = 0, 1, 2, 3, 4
+
+
+def wire_encode(msgs, wire_type):
+    """Data.Binary encoding (Common.hs:24,47,55) of pxb_msg records
+    (numpy uint32 (n, 4)) on the GPU.  Returns (bytes, offsets[n + 1])."""
+    import numpy as np
+    lib = load()
+    msgs = np.ascontiguousarray(msgs, dtype=np.uint32)
+    n = len(msgs)
+    out = np.zeros(max(1, n * WIRE_MAX_BYTES), dtype=np.uint8)
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    nb = C.c_uint64(0)
+    check(lib.pxb_wire_encode_host(_ptr(msgs), n, wire_type, _ptr(out), _ptr(offs), C.byref(nb)))
+    return out[:nb.value].tobytes(), offs
+
+
+def wire_decode(data: bytes, offsets, wire_type):
+    """Inverse of wire_encode: (msgs (n, 4) uint32, status (n,) uint32)."""
+    import numpy as np
+    lib = load()
+    offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+    n = len(offs) - 1
+    buf = np.frombuffer(data, dtype=np.uint8) if data else np.zeros(1, np.uint8)
+    buf = np.ascontiguousarray(buf)
+    msgs = np.zeros((max(n, 0), 4), dtype=np.uint32)
+    st = np.zeros(max(n, 0), dtype=np.uint32)
+    check(lib.pxb_wire_decode_host(_ptr(buf), _ptr(offs), n, wire_type, _ptr(msgs), _ptr(st)))
+    return msgs, st

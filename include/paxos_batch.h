@@ -184,6 +184,45 @@ int pxb_proposer_handle(pxb_proposer_rec* states, uint32_t n_acceptors,
                         const pxb_msg* msg, pxb_msg* bcast, uint32_t* n_bcast,
                         uint32_t count);
 
+/* ---- wire format ----------------------------------------
+ * Batch codec for the Data.Binary payloads the reference sends: the generic
+ * `instance Binary ClientRequest` / `instance Binary ServerResponse`
+ * (Common.hs:24,47,55; binary-0.8.5.1 from the lts-12.18 resolver): Word8
+ * constructor tag, Int = Int64 big-endian, Maybe = Word8 0|1 (+ value),
+ * Command = Int length + UTF-8 chars of "c<clientId>.<t>".  Messages use
+ * pxb_msg: requests kind 0/1/2 with x = ticket, z = command code
+ * ((clientId << 24) | t, Propose only); responses kind 0/1/2 with x = ticket,
+ * (y, z) = Round1OK's stored proposal (z == 0: Nothing).  A kind above 2
+ * encodes to an empty record.  Offsets are exclusive prefix sums
+ * (count + 1 entries): message i occupies bytes [off[i], off[i+1]).
+ * Replaces: Cloud Haskell's serialisation of `contentOf m` in sendMessages
+ * (Common.hs:36-39) for a batch of messages; the envelope (sender ProcessId,
+ * type fingerprint, TCP framing) is not part of it.                        */
+#define PXB_WIRE_REQUEST   0u     /* ClientRequest  (Common.hs:41-47)        */
+#define PXB_WIRE_RESPONSE  1u     /* ServerResponse (Common.hs:49-55)        */
+#define PXB_WIRE_MAX_BYTES 39     /* longest record: Round1OK with a Just    */
+/* per-message decode status */
+#define PXB_WIRE_OK        0u
+#define PXB_WIRE_E_LENGTH  1u     /* truncated record or trailing bytes      */
+#define PXB_WIRE_E_TAG     2u     /* constructor / Maybe tag out of range    */
+#define PXB_WIRE_E_STRING  3u     /* not a "c<id>.<t>" the reference prints  */
+#define PXB_WIRE_E_RANGE   4u     /* Int beyond int32, id > 255, t >= 2^24   */
+
+/* DEVICE buffers, asynchronous on `stream`.  pxb_wire_size writes the
+ * offsets of `count` encoded messages (d_offsets: count + 1 entries). */
+int pxb_wire_size(const pxb_msg* d_msgs, uint64_t count, uint32_t type, uint64_t* d_offsets, void* stream);
+int pxb_wire_encode(const pxb_msg* d_msgs, uint64_t count, uint32_t type, const uint64_t* d_offsets,
+                    uint8_t* d_bytes, void* stream);
+/* d_status (nullable): PXB_WIRE_* per message; failed messages decode to 0s */
+int pxb_wire_decode(const uint8_t* d_bytes, const uint64_t* d_offsets, uint64_t count, uint32_t type,
+                    pxb_msg* d_msgs, uint32_t* d_status, void* stream);
+/* HOST-buffer forms (blocking).  encode: `out` holds count * PXB_WIRE_MAX_BYTES
+ * bytes, offsets count + 1 entries, *nbytes = total bytes written. */
+int pxb_wire_encode_host(const pxb_msg* msgs, uint64_t count, uint32_t type, uint8_t* out, uint64_t* offsets,
+                         uint64_t* nbytes);
+int pxb_wire_decode_host(const uint8_t* in, const uint64_t* offsets, uint64_t count, uint32_t type,
+                         pxb_msg* msgs, uint32_t* status);
+
 /* ---- misc ----------------------------------------------------------------- */
 const char* pxb_strerror(int code);
 int         pxb_last_hip_error(void);
