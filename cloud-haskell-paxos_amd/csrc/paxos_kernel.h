@@ -200,6 +200,10 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
   constexpr uint32_t ZM = LOGM ? 0xFFFFu : 3u, KSH = LOGM ? 30u : 16u;
   using clog_t = typename Lds<PM, N, LOGM>::clog_t;
   constexpr uint32_t CB = LOGM ? 32u : 2u;    // epoch shift of a canonical-log entry
+  // A lone proposer on a fault-free schedule is never NACKed (its tickets only
+  // grow and nobody else raises T_max) and gets at most one response per link
+  // per step, so the NACK handling and the multi-response fold compile out.
+  constexpr bool CONTENDED = !(FF && PM == 1);
   __shared__ Lds<PM, N, LOGM> s_lds[WPB];
 
   const int lane = threadIdx.x & 63;
@@ -497,7 +501,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
             const bool mine = go && ((rem >> a) & 1u) != 0u;
             const bool is_ack = mine && ((rs == ROUND1 && kind == R1OK && x == T) ||
                                          (rs == ROUND2 && kind == R2S));
-            const bool is_ab = mine && rs != IDLE && kind == HAVE && x >= T;
+            const bool is_ab = CONTENDED && mine && rs != IDLE && kind == HAVE && x >= T;
             const uint32_t ackm = slot(ballot(is_ack));
             const uint32_t abm = slot(ballot(is_ab));
             const uint32_t need = (uint32_t)(N >> 1) + 1u - Sp.acks;
@@ -562,6 +566,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
           } while (any(go));
         }
         STAMP(3);
+#ifdef PXB_SERIAL_FOLD
         // ---- general path (a link holds >= 2 due responses): serial fold in
         // canonical order; every lane of the slot reads the head of lane aa's
         // link (ds_bpermute) and applies handleServerResponse; lane aa pops it.
@@ -594,6 +599,142 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
             }
           }
         }
+#else
+        // ---- multi path (some link of the slot holds >= 2 due responses).
+        // The canonical order is (acceptor a, link seq k); between events the
+        // proposer only counts acks, so the fold runs in rounds again, now over
+        // per-lane lists: every lane scans its own due responses (acks before
+        // its first qualifying NACK), a slot prefix sum of those counts finds
+        // the majority acceptor and the majority ack inside its list, the
+        // first NACK lane cuts the rest, MostRecent is a max over
+        // (t_store, -a, -k) of the counted proposals.  Same transitions as the
+        // fast path (Client.hs:128-189); all due responses are consumed.
+        const bool multi = pact && slot_serial;
+        if (CONTENDED && any(multi)) {
+          const uint32_t h0 = l_head(Sx[p]);
+          const uint32_t cntm = multi ? cnt_p : 0u;
+#pragma unroll 1
+          for (uint32_t k = 0; any(k < cntm); ++k) {          // canonical bytes of the consumed responses
+            const uint32_t w = L.sq[p][(h0 + k) & 7u][lane];
+            canon += (k < cntm) ? 2u * (16u >> (w >> 30)) : 0u;
+          }
+          uint32_t kp = 0;                                   // next unprocessed response of my list
+          bool go = multi;
+#pragma unroll 1
+          while (any(go)) {
+            PropState& Sp = S[p];
+            const uint32_t rs = Sp.rs;
+            const int32_t T = Sp.ticket;
+            // scan 1: acks before my first qualifying NACK, and that NACK
+            uint32_t c = 0, nk = 0xFFu;
+            int32_t ux = 0;
+#pragma unroll 1
+            for (uint32_t j = 0; any(go && kp + j < cntm && nk == 0xFFu); ++j) {
+              const uint32_t k = kp + j;
+              const bool v = go && k < cntm && nk == 0xFFu;
+              const uint32_t w = L.sq[p][(h0 + k) & 7u][lane];
+              const uint32_t kind = w >> 30;
+              const int32_t x = (int32_t)(w & 0x3FFFu);
+              const bool ack = v && ((rs == ROUND1 && kind == R1OK && x == T) || (rs == ROUND2 && kind == R2S));
+              const bool nack = v && rs != IDLE && kind == HAVE && x >= T;
+              c += ack ? 1u : 0u;
+              ux = nack ? x : ux;
+              nk = nack ? k : nk;
+            }
+            const uint32_t A = min(ffbl(slot(ballot(nk != 0xFFu))), ENONE);   // first NACK lane
+            const uint32_t ce = ((uint32_t)a <= A) ? c : 0u;
+            // inclusive prefix of ce over the slot's lanes (log-step shuffles)
+            uint32_t incl = ce;
+#pragma unroll
+            for (int off = 1; off < N; off <<= 1) {
+              const uint32_t o = (uint32_t)__shfl((int)incl, lane - off);
+              incl += (a >= off) ? o : 0u;
+            }
+            const uint32_t excl = incl - ce;
+            const uint32_t need = (uint32_t)(N >> 1) + 1u - Sp.acks;    // haveMajority, Client.hs:191-194
+            const bool majl = go && ce != 0u && excl < need && need <= incl;
+            const uint32_t M = min(ffbl(slot(ballot(majl))), ENONE);    // majority lane (<= A)
+            const bool mj = M != ENONE;
+            const uint32_t e = mj ? M : A;                              // event lane (ENONE: none)
+            const uint32_t r = need - excl;                             // majority = my r-th ack
+            // scan 2: the majority ack's index, and MostRecent candidates among
+            // the counted Round1OKs (lanes before the event: all; the event lane:
+            // up to the majority ack / before the NACK; no event: all)
+            uint32_t seen = 0, kmaj = 0, bkey = 0, bz = 0;
+            const bool r1 = rs == ROUND1;
+            if (any(go && (mj || r1))) {
+#pragma unroll 1
+              for (uint32_t j = 0; any(go && kp + j < cntm && kp + j < nk); ++j) {
+                const uint32_t k = kp + j;
+                const bool v = go && k < cntm && k < nk;
+                const uint32_t w = L.sq[p][(h0 + k) & 7u][lane];
+                const uint32_t kind = w >> 30;
+                const int32_t x = (int32_t)(w & 0x3FFFu);
+                const bool ack = v && ((r1 && kind == R1OK && x == T) || (rs == ROUND2 && kind == R2S));
+                seen += ack ? 1u : 0u;
+                const bool counted = ack && ((uint32_t)a < e || e == ENONE || ((uint32_t)a == e && (!mj || seen <= r)));
+                kmaj = (ack && seen == r) ? k : kmaj;
+                const uint32_t zc = LOGM ? L.sq2.w[p][(h0 + k) & 7u][lane] : ((w >> 28) & 3u);
+                const uint32_t y = (w >> 14) & 0x3FFFu;
+                const uint32_t key = (y << 8) | ((15u - (uint32_t)a) << 4) | (15u - k);
+                const bool el = counted && r1 && zc != 0u && key > bkey;
+                bkey = el ? key : bkey;
+                bz = el ? zc : bz;
+              }
+            }
+            // slot max of the candidates: DPP wave_shl:1 chain, result in lane base
+            uint32_t mkey = bkey;
+            if (any(bkey != 0u)) {
+#pragma unroll
+              for (int i = 1; i < N; ++i) {
+                const uint32_t nb = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mkey, 0x130, 0xF, 0xF, false);
+                mkey = (a + 1 < N) ? max(mkey, nb) : mkey;
+              }
+              mkey = (uint32_t)__shfl((int)mkey, base);
+            }
+            const uint32_t wz = (uint32_t)__shfl((int)bz, base + 15 - (int)((mkey >> 4) & 15u));
+            int32_t u = 0;
+            if (any(A != ENONE)) u = __shfl(ux, (A != ENONE) ? base + (int)A : lane);
+            const uint32_t total = (uint32_t)__shfl((int)incl, base + N - 1);   // acks counted, no event
+            // ---- the transition (Client.hs:128-189), as in the fast path ----
+            int32_t mt = Sp.mr_t;
+            uint32_t mv = Sp.mr_v;
+            const bool take = mkey != 0u && (mv == 0u || (int32_t)(mkey >> 8) > mt);
+            mt = take ? (int32_t)(mkey >> 8) : mt;
+            mv = take ? wz : mv;
+            const bool ev = go && e != ENONE;
+            const bool r1maj = ev && mj && rs == ROUND1;
+            const bool r2maj = ev && mj && rs == ROUND2;
+            const bool nack = ev && !mj;
+            const bool restart = r2maj && Sp.pending != 0u;
+            const bool idle = r2maj && Sp.pending == 0u;
+            const uint32_t r2v = (mv == 0u) ? Sp.cmd : mv;
+            const int32_t tn = nack ? u + 1 : T + 1;
+            const uint32_t k0o = r1maj ? PROPOSE : (r2maj ? EXECUTE : ASK);
+            const int32_t x0o = nack ? tn : T;
+            const uint32_t z0o = r1maj ? r2v : 0u;
+            Sp.r2_v = r1maj ? r2v : Sp.r2_v;
+            Sp.pending = r1maj ? ((mv != 0u) ? 1u : 0u) : Sp.pending;
+            Sp.ticket = (nack || restart) ? tn : T;
+            Sp.cmd = idle ? 0u : Sp.cmd;
+            Sp.acks = go ? (ev ? 0u : Sp.acks + total) : Sp.acks;
+            Sp.rs = r1maj ? ROUND2 : ((nack || restart) ? ROUND1 : (idle ? IDLE : rs));
+            const bool keep_mr = go && !ev && rs == ROUND1;
+            Sp.mr_t = keep_mr ? mt : (ev ? 0 : Sp.mr_t);
+            Sp.mr_v = keep_mr ? mv : (ev ? 0u : Sp.mr_v);
+            // consumed: lanes before the event lane all, the event lane through
+            // the event response, later lanes nothing; no event: everything
+            const uint32_t kev = (mj ? kmaj : nk) + 1u;
+            kp = !go ? kp : (e == ENONE || (uint32_t)a < e) ? cntm : ((uint32_t)a == e ? kev : kp);
+            if (any(ev)) send_req(pc, ev, k0o, x0o, z0o);
+            if (any(restart)) send_req(pc, restart, ASK, tn, 0u);
+            go = go && Sp.rs != IDLE && slot(ballot(kp < cntm)) != 0u;
+          }
+          // every due response has been consumed
+#pragma unroll 1
+          for (uint32_t k = 0; any(k < cntm); ++k) l_pop_if(Sx[p], k < cntm);
+        }
+#endif
       }
       canon += (stepped && a == 0) ? 48u : 0u;
       tovf = tovf || (pact && S[p].ticket >= PXB_TICKET_LIMIT);

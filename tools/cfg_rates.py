@@ -10,7 +10,10 @@ import pxb  # noqa: E402
 
 if len(sys.argv) > 1:
     pxb.load(os.path.join(ROOT, sys.argv[1]))
-for c, n, reps in ((2, 1 << 20, 10), (3, 1 << 22, 2), (4, 1 << 23, 2), (4, 1 << 26, 1), (5, 1 << 22, 1), (6, 1 << 20, 3)):
+CASES = ((2, 1 << 20, 10), (3, 1 << 22, 2), (4, 1 << 23, 2), (4, 1 << 26, 1), (5, 1 << 22, 1), (6, 1 << 20, 3))
+if os.environ.get("PXB_RATES_QUICK"):
+    CASES = tuple(c for c in CASES if c[1] <= (1 << 23))
+for c, n, reps in CASES:
     cfg = pxb.CONFIGS[c]
     N = cfg.n_acceptors
     out = torch.empty((n, 4), dtype=torch.int32, device="cuda")

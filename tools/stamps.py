@@ -13,7 +13,7 @@ import pxb  # noqa
 NAMES = ["refill", "acceptor", "prop_tick+count", "prop_fast", "prop_serial+tail", "endstep", "finish", "exit"]
 lib = pxb.load()
 lib.pxb_debug_stamps.argtypes = [C.c_void_p]
-for c, n in ((2, 1 << 20), (3, 1 << 22), (5, 1 << 20)):
+for c, n in ((2, 1 << 20), (3, 1 << 22), (4, 1 << 22), (5, 1 << 20)):
     cfg = pxb.CONFIGS[c]
     out = torch.zeros((n, 4), dtype=torch.int32, device="cuda")
     tot = torch.zeros(16, dtype=torch.int64, device="cuda")
