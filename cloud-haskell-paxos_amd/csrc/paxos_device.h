@@ -28,20 +28,9 @@ constexpr uint32_t IDLE = 0, ROUND1 = 1, ROUND2 = 2;
 // v_mul_lo_u32 + v_mul_hi_u32 pair.
 __device__ __forceinline__ uint4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                         uint32_t k0, uint32_t k1) {
-#ifdef PXB_PHILOX_CHEAP   // timing experiments only (similar statistics, NOT the schedule)
-  uint32_t h = c0 ^ (c1 * 0x9E3779B9u) ^ (c2 << 16) ^ (c2 >> 5) ^ (c3 * 0x85EBCA6Bu) ^ k0 ^ k1;
-  h ^= h >> 16; h += h << 3; h ^= h >> 11; h += h << 15; h ^= h >> 7; h += 0x632BE5ABu;
-  uint32_t g = h ^ 0x5bd1e995u; g ^= g >> 13; g += g << 7; g ^= g >> 17; g += g << 5;
-  return make_uint4(h, g, h ^ g, h + g);
-#endif
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-#if defined(PXB_PHILOX_MULHI)
-    const uint64_t p0 = ((uint64_t)__umulhi(0xD2511F53u, c0) << 32) | (0xD2511F53u * c0);
-    const uint64_t p1 = ((uint64_t)__umulhi(0xCD9E8D57u, c2) << 32) | (0xCD9E8D57u * c2);
-#else
     const uint64_t p0 = (uint64_t)c0 * 0xD2511F53u, p1 = (uint64_t)c2 * 0xCD9E8D57u;
-#endif
     const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
     c1 = (uint32_t)p1;
     c3 = (uint32_t)p0;

@@ -16,9 +16,10 @@
 //     slot.  Responses are folded in canonical (acceptor, link seq) order:
 //     quorum counting with __ballot + popcount, the majority acceptor from a
 //     prefix popcount, MostRecent (Common.hs:61-65) from a slot max-reduction;
-//     a serial ds_bpermute fold handles the rare slot with 2+ due responses on
-//     one link.  Each lane enqueues its own copy of a broadcast on its own
-//     link (Philox loss/delay per link, in parallel).
+//     a wave where some link holds 2+ due responses folds per-lane lists
+//     instead (lane scans + slot prefix sums + DPP max).  Each lane enqueues
+//     its own copy of a broadcast on its own link (Philox loss/delay per
+//     link, in parallel).
 //   * waves are persistent: when a slot's instance quiesces (or hits
 //     step_cap) the slot writes its 16-B result + 4-B/acceptor digests and
 //     refills from the wave's contiguous instance range.
@@ -148,6 +149,12 @@ __device__ __forceinline__ void l_pop_if(Link& L, bool p) {
   L.hl = p ? ((L.hl + 15u) & ~0x80u) : L.hl;
 }
 
+// pop n <= len entries at once
+__device__ __forceinline__ void l_pop_n(Link& L, uint32_t n) {
+  L.dn = (n >= 8u) ? 0u : (L.dn >> (4u * n));
+  L.hl = (L.hl & ~0x7Fu) | (((l_head(L) + n) & 7u) << 4) | (l_len(L) - n);
+}
+
 // Log mode (several Ticks per proposer, SEMANTICS §9) carries full commands
 // "c<id>.<t>" (16 bits: id << 14 | t) instead of the single-decree clientId:
 // a Round1OK then needs a second word, kept in a parallel ring.
@@ -183,6 +190,14 @@ template <> struct Occ<3> { static constexpr int waves = PXB_OCC_P3; };
 __device__ __forceinline__ uint4 philox_here(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                              uint32_t k0, uint32_t k1) {
   asm volatile("" : "+v"(c0), "+v"(c1), "+s"(k0), "+s"(k1));
+#ifdef PXB_PHILOX_TWICE_DIAG   // diagnostic: the marginal cost of the draws
+  {
+    uint32_t d0 = c0 ^ 1u;
+    asm volatile("" : "+v"(d0));
+    const uint4 w2 = philox(d0, c1, c2, c3, k0, k1);
+    asm volatile("" ::"v"(w2.x), "v"(w2.y));
+  }
+#endif
   return philox(c0, c1, c2, c3, k0, k1);
 }
 
@@ -469,7 +484,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
       if (anyb != 0ull) {
         const uint32_t mine_slot = slot(anyb);
         stepped = stepped || mine_slot != 0u;
-        const bool slot_serial = slot(ballot(cnt_p > 1u)) != 0u;
+        const bool slot_multi = slot(ballot(cnt_p > 1u)) != 0u;
         // ---- fast path: every link a -> p of the slot has <= 1 due response.
         // The serial fold of Client.hs:125-189 over acceptors 0..N-1 is done in
         // rounds, one per state-changing event (majority or NACK):
@@ -479,7 +494,11 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
         // an event only a NACK (not Idle) or a stale Round2Success (in Round2)
         // can still act: a fresh Round1OK for the new ticket cannot exist yet.
         // Every round is a select network (no divergent branches).
-        const bool fast = pact && !slot_serial && mine_slot != 0u;
+        // A wave with any multi slot runs every slot through the multi path
+        // (it is exact for <= 1 response per link too): the slots of a wave
+        // would otherwise pay for both paths.
+        const bool wave_multi = CONTENDED && any(pact && slot_multi);
+        const bool fast = pact && !wave_multi && mine_slot != 0u;
         if (any(fast)) {
           const bool has = fast && cnt_p == 1u;
           const uint32_t w = L.sq[p][l_head(Sx[p])][lane];
@@ -566,40 +585,6 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
           } while (any(go));
         }
         STAMP(3);
-#ifdef PXB_SERIAL_FOLD
-        // ---- general path (a link holds >= 2 due responses): serial fold in
-        // canonical order; every lane of the slot reads the head of lane aa's
-        // link (ds_bpermute) and applies handleServerResponse; lane aa pops it.
-        const uint32_t cnt_s = slot_serial ? cnt_p : 0u;
-        if (any(cnt_s > 0u)) {
-#pragma unroll 1
-          for (int aa = 0; aa < N; ++aa) {
-            uint32_t ca_ = (uint32_t)__shfl((int)cnt_s, base + aa);
-            while (any(ca_ > 0u)) {
-              const bool take = ca_ > 0u;
-              const uint32_t mine = L.sq[p][l_head(Sx[p])][lane];
-              const uint32_t w = (uint32_t)__shfl((int)mine, base + aa);
-              uint32_t z = (w >> 28) & 3u;
-              if (LOGM) z = (uint32_t)__shfl((int)L.sq2.w[p][l_head(Sx[p])][lane], base + aa);
-              Req o0{NONE, 0, 0}, o1{NONE, 0, 0};
-              uint32_t no = 0;
-              if (take) {
-                const uint32_t kind = w >> 30;
-                no = proposer_step(S[p], (uint32_t)N, kind, (int32_t)(w & 0x3FFFu),
-                                   (int32_t)((w >> 14) & 0x3FFFu), z, o0, o1);
-                if (a == aa) canon += 2u * (16u >> kind);
-                l_pop_if(Sx[p], a == aa);
-                ca_--;
-              }
-#pragma unroll 1
-              for (uint32_t k = 0; k < 2u; ++k) {
-                const bool hs = no > k;
-                if (any(hs)) send_req(pc, hs, k ? o1.kind : o0.kind, k ? o1.x : o0.x, k ? o1.z : o0.z);
-              }
-            }
-          }
-        }
-#else
         // ---- multi path (some link of the slot holds >= 2 due responses).
         // The canonical order is (acceptor a, link seq k); between events the
         // proposer only counts acks, so the fold runs in rounds again, now over
@@ -609,7 +594,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
         // first NACK lane cuts the rest, MostRecent is a max over
         // (t_store, -a, -k) of the counted proposals.  Same transitions as the
         // fast path (Client.hs:128-189); all due responses are consumed.
-        const bool multi = pact && slot_serial;
+        const bool multi = pact && wave_multi && mine_slot != 0u;
         if (CONTENDED && any(multi)) {
           const uint32_t h0 = l_head(Sx[p]);
           const uint32_t cntm = multi ? cnt_p : 0u;
@@ -730,11 +715,8 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
             if (any(restart)) send_req(pc, restart, ASK, tn, 0u);
             go = go && Sp.rs != IDLE && slot(ballot(kp < cntm)) != 0u;
           }
-          // every due response has been consumed
-#pragma unroll 1
-          for (uint32_t k = 0; any(k < cntm); ++k) l_pop_if(Sx[p], k < cntm);
+          l_pop_n(Sx[p], cntm);                              // every due response is consumed
         }
-#endif
       }
       canon += (stepped && a == 0) ? 48u : 0u;
       tovf = tovf || (pact && S[p].ticket >= PXB_TICKET_LIMIT);
