@@ -145,12 +145,12 @@ extern "C" {
 int pxb_abi_version(void) { return PXB_ABI_VERSION; }
 
 #ifdef PXB_STAMPS
-// diagnostic build only: cycles per kernel section summed over waves (and reset)
-int pxb_debug_stamps(unsigned long long* out8) {
+// diagnostic build only: cycles per kernel section and event counts, summed over waves (and reset)
+int pxb_debug_stamps(unsigned long long* out16) {
   if (!g_dbg) return PXB_E_INVAL;
   HIPCHK(hipDeviceSynchronize());
-  HIPCHK(hipMemcpy(out8, g_dbg, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-  HIPCHK(hipMemset(g_dbg, 0, 8 * sizeof(unsigned long long)));
+  HIPCHK(hipMemcpy(out16, g_dbg, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemset(g_dbg, 0, 16 * sizeof(unsigned long long)));
   return PXB_OK;
 }
 #endif
@@ -235,8 +235,8 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
   {
     static unsigned long long* dbg = nullptr;
     if (!dbg) {
-      HIPCHK(hipMalloc(&dbg, 8 * sizeof(unsigned long long)));
-      HIPCHK(hipMemset(dbg, 0, 8 * sizeof(unsigned long long)));
+      HIPCHK(hipMalloc(&dbg, 16 * sizeof(unsigned long long)));
+      HIPCHK(hipMemset(dbg, 0, 16 * sizeof(unsigned long long)));
     }
     kp.dbg = dbg;
     g_dbg = dbg;

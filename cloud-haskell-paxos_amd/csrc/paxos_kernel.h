@@ -103,7 +103,11 @@ __device__ __forceinline__ void static_for(F&& f) {
 
 // ---- diagnostic section stamps (separate build: -DPXB_STAMPS; never timed) --
 #ifdef PXB_STAMPS
-#define STAMP_DECL uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; uint64_t st_prev = __builtin_amdgcn_s_memtime();
+#define STAMP_DECL                                                \
+  uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};                  \
+  uint32_t st_cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};                  \
+  uint64_t st_prev = __builtin_amdgcn_s_memtime();
+#define SCOUNT(i) (st_cnt[i]++)
 #define STAMP(i)                                                  \
   do {                                                            \
     __builtin_amdgcn_sched_barrier(0);                            \
@@ -115,10 +119,12 @@ __device__ __forceinline__ void static_for(F&& f) {
 #define STAMP_FLUSH(ptr)                                          \
   if (lane == 0 && (ptr)) {                                       \
     for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&(ptr)[i_], (unsigned long long)st_acc[i_]); \
+    for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&(ptr)[8 + i_], (unsigned long long)st_cnt[i_]); \
   }
 #else
 #define STAMP_DECL
 #define STAMP(i) do {} while (0)
+#define SCOUNT(i) do {} while (0)
 #define STAMP_FLUSH(ptr)
 #endif
 
@@ -279,15 +285,20 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
     Sx[p] = Link{0, 0, 0};
   }
 
+  STAMP_DECL
   // common link send, predicated on `pred` (docs/SEMANTICS.md §5): Philox
-  // loss/delay, FIFO due, bounded ring (overflow -> flag, message dropped)
+  // loss/delay, FIFO due, bounded ring (overflow -> flag, message dropped);
+  // returns whether the message was queued
   auto link_send = [&](Link& Lk, uint32_t* ring, uint32_t* ring2, uint32_t dirbits, uint32_t word,
-                       uint32_t word2, bool pred) {
+                       uint32_t word2, bool pred) -> bool {
     msgs_acc += pred ? 1u : 0u;
     const uint32_t k = Lk.seq;
     Lk.seq = pred ? k + 1u : k;
     int32_t d = 1;
     bool ok = true;
+#ifdef PXB_STAMPS
+    if (!FF && any(pred && faulty)) SCOUNT(5);
+#endif
     if (!FF && pred && faulty) {
       const uint64_t inst = kp.first_instance + idx;
       const uint4 w = philox_here((uint32_t)inst, (uint32_t)(inst >> 32), k, (1u << 24) | dirbits | (uint32_t)a, k0, k1);
@@ -311,6 +322,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
       Lk.dn = push ? (Lk.dn | (((uint32_t)due & 15u) << (4u * len))) : Lk.dn;
       Lk.hl = push ? (((Lk.hl & 0x7Fu) + 1u) | ((uint32_t)due << 8)) : Lk.hl;
     }
+    return push;
   };
   // proposer p's broadcast copy on link p -> a (sendToAllServers, Client.hs:122-123)
   auto send_req = [&](auto pc, bool has, uint32_t kind, int32_t x, uint32_t z) {
@@ -357,12 +369,17 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
     // tickets are < 2^14 (SEMANTICS §6), so the fields need no masking
     // (log mode: the clientId field says Just / Nothing, the full command
     // travels in the second ring)
-    link_send(Sx[p], &L.sq[p][0][0], LOGM ? &L.sq2.w[p][0][0] : nullptr, (1u << 16) | ((uint32_t)p << 8),
-              (uint32_t)rx | ((uint32_t)ry << 14) | ((LOGM ? (rz >> 14) : rz) << 28) | (rk << 30), rz,
-              rk != NONE);
+    const bool queued =
+        link_send(Sx[p], &L.sq[p][0][0], LOGM ? &L.sq2.w[p][0][0] : nullptr, (1u << 16) | ((uint32_t)p << 8),
+                  (uint32_t)rx | ((uint32_t)ry << 14) | ((LOGM ? (rz >> 14) : rz) << 28) | (rk << 30), rz,
+                  rk != NONE);
+    // a queued response is charged here as delivered (payload written + read,
+    // Round1OK 16, HaveTicket 8, Round2Success 4 B): every queued response is
+    // consumed before quiescence, and a step-capped instance gives back the
+    // ones still queued when it stops
+    canon += queued ? 2u * (16u >> (rk & 3u)) : 0u;
   };
 
-  STAMP_DECL
   for (;;) {
     // ---------------- refill free slots from this wave's range -------------
     const uint64_t freeb = ballot(used && !active && a == 0);
@@ -427,6 +444,10 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
       next = min(next + (uint32_t)__popcll(freeb), end);
     }
     if (!any(active)) break;
+    SCOUNT(0);
+#ifdef PXB_STAMPS
+    st_cnt[7] += (uint32_t)__popcll(ballot(active && a == 0));
+#endif
     STAMP(0);
 
     const uint32_t srep = ((uint32_t)s & 15u) * 0x11111111u;
@@ -446,6 +467,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
         uint32_t cnt = active ? (FF ? l_len(R[p]) : l_due_count(R[p], srep)) : 0u;
         if (any(cnt > 0u)) {
           do {
+            SCOUNT(1);
             acc_take(pc, cnt > 0u, isolated);
             cnt = (cnt > 0u) ? cnt - 1u : 0u;
           } while (any(cnt > 0u));
@@ -508,12 +530,12 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
           const int32_t x = (int32_t)(w & 0x3FFFu);
           const int32_t y = (int32_t)((w >> 14) & 0x3FFFu);
           const uint32_t z = has ? (LOGM ? w2 : ((w >> 28) & 3u)) : 0u;
-          canon += has ? 2u * (16u >> kind) : 0u;
           uint32_t rem = slot(ballot(has));                 // unprocessed responses
           const uint32_t havem = slot(ballot(kind == HAVE));
           const uint32_t r2sm = slot(ballot(kind == R2S));
           bool go = fast;
           do {
+            SCOUNT(2);
             PropState& Sp = S[p];
             const uint32_t rs = Sp.rs;
             const int32_t T = Sp.ticket;
@@ -596,22 +618,22 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
         // fast path (Client.hs:128-189); all due responses are consumed.
         const bool multi = pact && wave_multi && mine_slot != 0u;
         if (CONTENDED && any(multi)) {
+          SCOUNT(3);
           const uint32_t h0 = l_head(Sx[p]);
           const uint32_t cntm = multi ? cnt_p : 0u;
-#pragma unroll 1
-          for (uint32_t k = 0; any(k < cntm); ++k) {          // canonical bytes of the consumed responses
-            const uint32_t w = L.sq[p][(h0 + k) & 7u][lane];
-            canon += (k < cntm) ? 2u * (16u >> (w >> 30)) : 0u;
-          }
           uint32_t kp = 0;                                   // next unprocessed response of my list
           bool go = multi;
 #pragma unroll 1
           while (any(go)) {
+            SCOUNT(4);
             PropState& Sp = S[p];
             const uint32_t rs = Sp.rs;
             const int32_t T = Sp.ticket;
-            // scan 1: acks before my first qualifying NACK, and that NACK
-            uint32_t c = 0, nk = 0xFFu;
+            // scan: acks before my first qualifying NACK (count and position
+            // mask), that NACK, and the best MostRecent candidate among those
+            // acks, key (t_store, -a, -k)
+            const bool r1 = rs == ROUND1;
+            uint32_t c = 0, nk = 0xFFu, ackb = 0, bkey = 0, bz = 0;
             int32_t ux = 0;
 #pragma unroll 1
             for (uint32_t j = 0; any(go && kp + j < cntm && nk == 0xFFu); ++j) {
@@ -620,11 +642,17 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
               const uint32_t w = L.sq[p][(h0 + k) & 7u][lane];
               const uint32_t kind = w >> 30;
               const int32_t x = (int32_t)(w & 0x3FFFu);
-              const bool ack = v && ((rs == ROUND1 && kind == R1OK && x == T) || (rs == ROUND2 && kind == R2S));
+              const bool ack = v && ((r1 && kind == R1OK && x == T) || (rs == ROUND2 && kind == R2S));
               const bool nack = v && rs != IDLE && kind == HAVE && x >= T;
               c += ack ? 1u : 0u;
+              ackb |= ack ? (1u << k) : 0u;
               ux = nack ? x : ux;
               nk = nack ? k : nk;
+              const uint32_t zc = LOGM ? L.sq2.w[p][(h0 + k) & 7u][lane] : ((w >> 28) & 3u);
+              const uint32_t key = (((w >> 14) & 0x3FFFu) << 8) | ((15u - (uint32_t)a) << 4) | (15u - k);
+              const bool el = ack && r1 && zc != 0u && key > bkey;
+              bkey = el ? key : bkey;
+              bz = el ? zc : bz;
             }
             const uint32_t A = min(ffbl(slot(ballot(nk != 0xFFu))), ENONE);   // first NACK lane
             const uint32_t ce = ((uint32_t)a <= A) ? c : 0u;
@@ -642,30 +670,36 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
             const bool mj = M != ENONE;
             const uint32_t e = mj ? M : A;                              // event lane (ENONE: none)
             const uint32_t r = need - excl;                             // majority = my r-th ack
-            // scan 2: the majority ack's index, and MostRecent candidates among
-            // the counted Round1OKs (lanes before the event: all; the event lane:
-            // up to the majority ack / before the NACK; no event: all)
-            uint32_t seen = 0, kmaj = 0, bkey = 0, bz = 0;
-            const bool r1 = rs == ROUND1;
-            if (any(go && (mj || r1))) {
+            // the majority ack's index: the r-th set bit of the ack mask
+            // (r <= need <= N/2 + 1 <= 5)
+            uint32_t bits = ackb;
+#pragma unroll
+            for (uint32_t i = 1; i < 5u; ++i) bits = (i < r) ? (bits & (bits - 1u)) : bits;
+            const uint32_t kmaj = ffbl(bits);
+            // MostRecent counts the acks of the lanes before the event lane (all
+            // lanes when there is none) and of the event lane up to its majority
+            // ack or its NACK (where the scan stopped).  Only an event lane with
+            // acks after its majority ack needs a shorter candidate scan: it has
+            // 2+ acks, which a Round1 list never holds (one Round1OK per Ask,
+            // tickets strictly increase) but the fold stays exact regardless.
+            const bool counted_lane = go && ((uint32_t)a < e || e == ENONE || (uint32_t)a == e);
+            const bool redo = go && r1 && mj && (uint32_t)a == e && c > r;
+            bkey = counted_lane ? bkey : 0u;
+            if (any(redo)) {
+              uint32_t rk2 = 0, rz2 = 0;
 #pragma unroll 1
-              for (uint32_t j = 0; any(go && kp + j < cntm && kp + j < nk); ++j) {
+              for (uint32_t j = 0; any(redo && kp + j <= kmaj); ++j) {
                 const uint32_t k = kp + j;
-                const bool v = go && k < cntm && k < nk;
+                const bool v = redo && k <= kmaj && ((ackb >> k) & 1u) != 0u;
                 const uint32_t w = L.sq[p][(h0 + k) & 7u][lane];
-                const uint32_t kind = w >> 30;
-                const int32_t x = (int32_t)(w & 0x3FFFu);
-                const bool ack = v && ((r1 && kind == R1OK && x == T) || (rs == ROUND2 && kind == R2S));
-                seen += ack ? 1u : 0u;
-                const bool counted = ack && ((uint32_t)a < e || e == ENONE || ((uint32_t)a == e && (!mj || seen <= r)));
-                kmaj = (ack && seen == r) ? k : kmaj;
                 const uint32_t zc = LOGM ? L.sq2.w[p][(h0 + k) & 7u][lane] : ((w >> 28) & 3u);
-                const uint32_t y = (w >> 14) & 0x3FFFu;
-                const uint32_t key = (y << 8) | ((15u - (uint32_t)a) << 4) | (15u - k);
-                const bool el = counted && r1 && zc != 0u && key > bkey;
-                bkey = el ? key : bkey;
-                bz = el ? zc : bz;
+                const uint32_t key = (((w >> 14) & 0x3FFFu) << 8) | ((15u - (uint32_t)a) << 4) | (15u - k);
+                const bool el = v && zc != 0u && key > rk2;
+                rk2 = el ? key : rk2;
+                rz2 = el ? zc : rz2;
               }
+              bkey = redo ? rk2 : bkey;
+              bz = redo ? rz2 : bz;
             }
             // slot max of the candidates: DPP wave_shl:1 chain, result in lane base
             uint32_t mkey = bkey;
@@ -720,8 +754,8 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
       }
       canon += (stepped && a == 0) ? 48u : 0u;
       tovf = tovf || (pact && S[p].ticket >= PXB_TICKET_LIMIT);
+      STAMP(4);
     });
-    STAMP(4);
 
     // ---------------- end of step: quiescence / step cap ---------------------
     uint32_t lens = 0;
@@ -733,7 +767,19 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
     s += active ? 1 : 0;
     const bool done = quiet || cap;
     STAMP(5);
+    if (any(cap)) {                             // responses charged but never delivered
+#pragma unroll
+      for (int p = 0; p < PM; ++p) {
+        const uint32_t len = cap ? l_len(Sx[p]) : 0u;
+#pragma unroll 1
+        for (uint32_t k = 0; any(k < len); ++k) {
+          const uint32_t w = L.sq[p][(l_head(Sx[p]) + k) & 7u][lane];
+          canon -= (k < len) ? 2u * (16u >> (w >> 30)) : 0u;
+        }
+      }
+    }
     if (any(done)) {
+      SCOUNT(6);
       const uint32_t pan = slot(ballot(A.dead));             // Q6: dead <=> panicked
       const uint32_t dvg = slot(ballot((lflags & PXB_F_LOG_DIVERGENCE) != 0u));
       const uint32_t qov = slot(ballot((lflags & PXB_F_QUEUE_OVERFLOW) != 0u));
