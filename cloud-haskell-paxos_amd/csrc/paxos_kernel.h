@@ -337,12 +337,12 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
     }
     link_send(R[p], &L.rq[p][0][0], nullptr, (uint32_t)p << 8, (uint32_t)x | (z << 14) | (kind << KSH), 0u, has);
   };
-  // one request from the head of link p -> a, predicated on `due`:
-  // handleClientRequest, Server.hs:51-78 (dead / isolated acceptors discard it)
-  auto acc_take = [&](auto pc, bool due, bool isolated) {
-    constexpr int p = decltype(pc)::value;
-    const uint32_t w = L.rq[p][l_head(R[p])][lane];
-    l_pop_if(R[p], due);
+  // one request from the head of link p -> a (Rl; the reply goes on Sl,
+  // link a -> p), predicated on `due`: handleClientRequest, Server.hs:51-78
+  // (dead / isolated acceptors discard it).  p may differ between lanes.
+  auto acc_take = [&](Link& Rl, Link& Sl, uint32_t p, bool due, bool isolated) {
+    const uint32_t w = (&L.rq[0][0][0])[(p * QD + l_head(Rl)) * 64u + (uint32_t)lane];
+    l_pop_if(Rl, due);
     const uint32_t kind = (w >> KSH) & 3u;
     const bool live = due && !A.dead && !isolated;
     const uint32_t rb = 8u + ((kind & 1u) << 2);       // payload: Propose 12, Ask / Execute 8
@@ -370,7 +370,8 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
     // (log mode: the clientId field says Just / Nothing, the full command
     // travels in the second ring)
     const bool queued =
-        link_send(Sx[p], &L.sq[p][0][0], LOGM ? &L.sq2.w[p][0][0] : nullptr, (1u << 16) | ((uint32_t)p << 8),
+        link_send(Sl, &L.sq[0][0][0] + p * (QD * 64u), LOGM ? &L.sq2.w[0][0][0] + p * (QD * 64u) : nullptr,
+                  (1u << 16) | (p << 8),
                   (uint32_t)rx | ((uint32_t)ry << 14) | ((LOGM ? (rz >> 14) : rz) << 28) | (rk << 30), rz,
                   rk != NONE);
     // a queued response is charged here as delivered (payload written + read,
@@ -457,22 +458,61 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
 #pragma unroll
     for (int p = 0; p < PM; ++p) sx_due[p] = FF ? l_len(Sx[p]) : 0u;
     // ---------------- acceptor phase: (proposer index, link seq) order -------
-    // handleClientRequest, Server.hs:51-78, for every due request of lane a;
-    // the first due request of every lane is handled straight-line, further
-    // ones (delay > 1 bunching) in a loop.
+    // handleClientRequest, Server.hs:51-78, for every due request of lane a,
+    // one request per lane per iteration (predicated, no divergent branches)
     {
       const bool isolated = !FF && (c0 <= s) && (s < c1);
-      static_for<0, PM>([&](auto pc) {
-        constexpr int p = decltype(pc)::value;
-        uint32_t cnt = active ? (FF ? l_len(R[p]) : l_due_count(R[p], srep)) : 0u;
+      if constexpr (PM == 1) {
+        uint32_t cnt = active ? (FF ? l_len(R[0]) : l_due_count(R[0], srep)) : 0u;
         if (any(cnt > 0u)) {
           do {
             SCOUNT(1);
-            acc_take(pc, cnt > 0u, isolated);
+            acc_take(R[0], Sx[0], 0u, cnt > 0u, isolated);
             cnt = (cnt > 0u) ? cnt - 1u : 0u;
           } while (any(cnt > 0u));
         }
-      });
+      } else {
+        // every lane walks its own (p, seq) list, so the wave iterates
+        // max over lanes of the lane's total, not the sum over p of per-link
+        // maxima; the link of the current request is selected per lane
+        uint32_t cn[PM];
+        uint32_t left = 0;
+#pragma unroll
+        for (int p = 0; p < PM; ++p) {
+          cn[p] = active ? (FF ? l_len(R[p]) : l_due_count(R[p], srep)) : 0u;
+          left += cn[p];
+        }
+        if (any(left > 0u)) {
+          do {
+            SCOUNT(1);
+            uint32_t ps = PM - 1;
+#pragma unroll
+            for (int p = PM - 2; p >= 0; --p) ps = (cn[p] != 0u) ? (uint32_t)p : ps;
+            Link Rl = R[PM - 1], Sl = Sx[PM - 1];
+#pragma unroll
+            for (int p = 0; p < PM - 1; ++p) {
+              Rl.dn = (ps == (uint32_t)p) ? R[p].dn : Rl.dn;
+              Rl.hl = (ps == (uint32_t)p) ? R[p].hl : Rl.hl;
+              Sl.dn = (ps == (uint32_t)p) ? Sx[p].dn : Sl.dn;
+              Sl.hl = (ps == (uint32_t)p) ? Sx[p].hl : Sl.hl;
+              Sl.seq = (ps == (uint32_t)p) ? Sx[p].seq : Sl.seq;
+            }
+            const bool due = left > 0u;
+            acc_take(Rl, Sl, ps, due, isolated);
+#pragma unroll
+            for (int p = 0; p < PM; ++p) {
+              const bool me = due && ps == (uint32_t)p;
+              R[p].dn = me ? Rl.dn : R[p].dn;
+              R[p].hl = me ? Rl.hl : R[p].hl;
+              Sx[p].dn = me ? Sl.dn : Sx[p].dn;
+              Sx[p].hl = me ? Sl.hl : Sx[p].hl;
+              Sx[p].seq = me ? Sl.seq : Sx[p].seq;
+              cn[p] -= me ? 1u : 0u;
+            }
+            left -= due ? 1u : 0u;
+          } while (any(left > 0u));
+        }
+      }
     }
     STAMP(1);
 
