@@ -118,9 +118,10 @@ def traffic_per_launch(c, n):
 def wire_bench(stream, dev, n=1 << 24, reps=5):
     """Wire codec: Data.Binary encode / decode of n
     ServerResponse records resident in HBM (a Round1OK-heavy mix with real
-    commands), HIP events on the launch stream.  HBM bytes per message:
-    encode 16 (pxb_msg) + 8 (offset) + record; decode record + 16 offset
-    reads + 16 (pxb_msg) + 4 (status)."""
+    commands), HIP events on the launch stream.  Algorithmic HBM bytes per
+    message: encode (sizes, offsets and records in one call) 16 (pxb_msg) +
+    8 (offset) + record; decode record + 16 offset reads + 16 (pxb_msg) + 4
+    (status)."""
     import numpy as np
     rng = np.random.default_rng(0)
     kind = rng.choice([0, 0, 1, 2], size=n).astype(np.uint32)
@@ -139,9 +140,8 @@ def wire_bench(stream, dev, n=1 << 24, reps=5):
     sp = stream.cuda_stream
     ptr = lambda t: pxb.C.c_void_p(t.data_ptr())  # noqa: E731
 
-    def enc():
-        pxb.check(lib.pxb_wire_size(ptr(d_m), n, pxb.WIRE_RESPONSE, ptr(d_o), pxb.C.c_void_p(sp)))
-        pxb.check(lib.pxb_wire_encode(ptr(d_m), n, pxb.WIRE_RESPONSE, ptr(d_o), ptr(d_b), pxb.C.c_void_p(sp)))
+    def enc():   # fused size + encode (pxb_wire_encode_all)
+        pxb.wire_encode_device(d_m, pxb.WIRE_RESPONSE, d_o, d_b, stream=sp)
 
     def dec():
         pxb.check(lib.pxb_wire_decode(ptr(d_b), ptr(d_o), n, pxb.WIRE_RESPONSE, ptr(d_back), ptr(d_st),

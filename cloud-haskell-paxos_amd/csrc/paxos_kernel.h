@@ -447,6 +447,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
     if (!any(active)) break;
     SCOUNT(0);
 #ifdef PXB_STAMPS
+    uint32_t st_sr = 0;   // this slot's fold rounds over all proposers this step
     st_cnt[7] += (uint32_t)__popcll(ballot(active && a == 0));
 #endif
     STAMP(0);
@@ -576,6 +577,9 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
           bool go = fast;
           do {
             SCOUNT(2);
+#ifdef PXB_STAMPS
+            st_sr += go ? 1u : 0u;
+#endif
             PropState& Sp = S[p];
             const uint32_t rs = Sp.rs;
             const int32_t T = Sp.ticket;
@@ -666,6 +670,9 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
 #pragma unroll 1
           while (any(go)) {
             SCOUNT(4);
+#ifdef PXB_STAMPS
+            st_sr += go ? 1u : 0u;
+#endif
             PropState& Sp = S[p];
             const uint32_t rs = Sp.rs;
             const int32_t T = Sp.ticket;
@@ -796,6 +803,13 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
       tovf = tovf || (pact && S[p].ticket >= PXB_TICKET_LIMIT);
       STAMP(4);
     });
+#ifdef PXB_STAMPS
+    {
+      uint32_t m = st_sr;
+      for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off));
+      st_cnt[6] += m;
+    }
+#endif
 
     // ---------------- end of step: quiescence / step cap ---------------------
     uint32_t lens = 0;
@@ -819,7 +833,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
       }
     }
     if (any(done)) {
-      SCOUNT(6);
+
       const uint32_t pan = slot(ballot(A.dead));             // Q6: dead <=> panicked
       const uint32_t dvg = slot(ballot((lflags & PXB_F_LOG_DIVERGENCE) != 0u));
       const uint32_t qov = slot(ballot((lflags & PXB_F_QUEUE_OVERFLOW) != 0u));

@@ -9,10 +9,17 @@
 // Maybe = Word8 0 | 1 + value, String = Int length + UTF-8 chars.  Restated
 // and pinned in oracle/wire_ref.py.
 //
-// One thread per message.  Sizes -> exclusive offsets (hipCUB scan) ->
-// bytes; decoding takes the offsets (the transport frames every message) and
-// reports a status per message.  HBM-bound byte work: 16 B of pxb_msg plus
-// 1..39 B of wire bytes per message.
+// One thread per message.  Sizes: one hipCUB scan over the record sizes
+// computed on the fly (no size pass in HBM).  Encoding: a tile of ETILE
+// messages builds its records in LDS at their tile-local offsets (block scan
+// of the sizes, one global offset per tile) and writes the tile's contiguous
+// byte range with aligned 16-B stores.  pxb_wire_encode_all fuses the two:
+// per-tile size sums, a scan of those, then the encode tiles also write the
+// offsets (HBM: the messages twice, offsets and bytes once).  Decoding stages the tile's byte range
+// through LDS with aligned 16-B loads and parses from LDS (records outside a
+// well-formed tile range are parsed straight from HBM).  Every message gets a
+// status.  HBM-bound byte work: 16 B of pxb_msg plus 1..39 B of wire bytes per
+// message.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -46,11 +53,41 @@ __device__ __forceinline__ uint32_t record_size(const pxb_msg& m, uint32_t type)
   return (m.kind == HAVE) ? 9u : 1u;
 }
 
-__global__ void size_kernel(const pxb_msg* __restrict__ msgs, uint64_t n, uint32_t type,
-                            uint64_t* __restrict__ offs) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i == 0) offs[0] = 0;
-  if (i < n) offs[i + 1] = record_size(msgs[i], type);
+// messages per block, one per thread (measured: small encode tiles overlap
+// their scan / LDS / store phases better; decode prefers long staged ranges)
+constexpr int ETILE = 256;
+constexpr int DTILE = 1024;
+// LDS stage of a tile's bytes in uint4: worst case + the alignment head
+template <int T> struct Stage { static constexpr int n = (T * PXB_WIRE_MAX_BYTES + 16 + 15) / 16; };
+
+struct SizeOp {
+  uint32_t type;
+  __device__ __forceinline__ uint64_t operator()(const pxb_msg& m) const { return record_size(m, type); }
+};
+
+// inclusive scan over the threads of a T-thread block (wave scans + LDS)
+template <int T>
+__device__ __forceinline__ uint32_t block_scan(uint32_t v, uint32_t* s_w, uint32_t& total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t o = (uint32_t)__shfl_up((int)v, off);
+    v += (lane >= off) ? o : 0u;
+  }
+  if (lane == 63) s_w[w] = v;
+  __syncthreads();
+  if (w == 0) {
+    uint32_t t = (lane < T / 64) ? s_w[lane] : 0u;
+#pragma unroll
+    for (int off = 1; off < T / 64; off <<= 1) {
+      const uint32_t o = (uint32_t)__shfl_up((int)t, off);
+      t += (lane >= off) ? o : 0u;
+    }
+    if (lane < T / 64) s_w[lane] = t;
+  }
+  __syncthreads();
+  total = s_w[T / 64 - 1];
+  return v + (w ? s_w[w - 1] : 0u);
 }
 
 struct Out {
@@ -78,13 +115,7 @@ struct Out {
   }
 };
 
-__global__ void encode_kernel(const pxb_msg* __restrict__ msgs, uint64_t n, uint32_t type,
-                              const uint64_t* __restrict__ offs, uint8_t* __restrict__ bytes) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const pxb_msg m = msgs[i];
-  if (m.kind > 2u) return;
-  Out o{bytes + offs[i]};
+__device__ __forceinline__ void encode_record(Out& o, const pxb_msg& m, uint32_t type) {
   o.u8(m.kind);                                          // constructor tag
   if (type == PXB_WIRE_REQUEST) {
     o.i64(m.x);                                          // the Ticket of every request
@@ -100,6 +131,78 @@ __global__ void encode_kernel(const pxb_msg* __restrict__ msgs, uint64_t n, uint
     }
   } else if (m.kind == HAVE) {
     o.i64(m.x);
+  }
+}
+
+// sum of the record sizes of every ETILE-message tile (encode_all pass 1); a
+// block covers SUM_TILES tiles so every thread keeps that many loads in flight
+constexpr int SUM_TILES = 4;
+__global__ __launch_bounds__(ETILE) void tile_sum_kernel(const pxb_msg* __restrict__ msgs, uint64_t n, uint32_t type,
+                                                         uint64_t ntiles, uint64_t* __restrict__ tsum) {
+  __shared__ uint32_t s_w[SUM_TILES][ETILE / 64];
+  const uint64_t t0 = (uint64_t)blockIdx.x * SUM_TILES;
+  pxb_msg m[SUM_TILES];
+#pragma unroll
+  for (int j = 0; j < SUM_TILES; ++j) {
+    const uint64_t i = (t0 + j) * ETILE + threadIdx.x;
+    m[j] = (i < n) ? msgs[i] : pxb_msg{3u, 0, 0, 0};
+  }
+#pragma unroll
+  for (int j = 0; j < SUM_TILES; ++j) {
+    uint32_t v = (m[j].kind <= 2u) ? record_size(m[j], type) : 0u;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += (uint32_t)__shfl_xor((int)v, off);
+    if ((threadIdx.x & 63) == 0) s_w[j][threadIdx.x >> 6] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < SUM_TILES && t0 + threadIdx.x < ntiles) {
+    uint32_t t = 0;
+#pragma unroll
+    for (int w = 0; w < ETILE / 64; ++w) t += s_w[threadIdx.x][w];
+    tsum[t0 + threadIdx.x] = t;
+  }
+}
+
+// One tile: records built in LDS, then the tile's byte range [base, base +
+// total) written with aligned 16-B stores (byte stores only for the partial
+// 16-B chunks at its two ends, which neighbouring tiles share).  The tile's
+// base is offs[first] (pxb_wire_encode) or the scanned tile sum, in which case
+// the tile also writes its offsets (pxb_wire_encode_all).
+template <bool WRITE_OFFS>
+__global__ __launch_bounds__(ETILE) void encode_kernel(const pxb_msg* __restrict__ msgs, uint64_t n, uint32_t type,
+                                                       uint64_t* __restrict__ offs, const uint64_t* __restrict__ toff,
+                                                       uint8_t* __restrict__ bytes) {
+  __shared__ uint4 s_buf[Stage<ETILE>::n];
+  __shared__ uint32_t s_w[ETILE / 64];
+  uint8_t* buf = reinterpret_cast<uint8_t*>(s_buf);
+  const uint64_t first = (uint64_t)blockIdx.x * ETILE;
+  const uint64_t i = first + threadIdx.x;
+  pxb_msg m{3u, 0, 0, 0};
+  if (i < n) m = msgs[i];
+  const uint32_t sz = (m.kind <= 2u) ? record_size(m, type) : 0u;
+  uint32_t total;
+  const uint32_t loc = block_scan<ETILE>(sz, s_w, total) - sz;
+  const uint64_t base = WRITE_OFFS ? toff[blockIdx.x] : offs[first];
+  if (WRITE_OFFS) {
+    if (i < n) offs[i + 1] = base + loc + sz;
+    if (i == 0) offs[0] = 0;
+  }
+  uint8_t* gdst = bytes + base;
+  const uint32_t pad = (uint32_t)((uintptr_t)gdst & 15u);  // LDS byte k <-> global gdst - pad + k
+  if (sz) {
+    Out o{buf + pad + loc};
+    encode_record(o, m, type);
+  }
+  __syncthreads();
+  const uint32_t span = pad + total;
+  uint8_t* g0 = gdst - pad;                              // 16-B aligned
+  for (uint32_t c = threadIdx.x; c * 16u < span; c += ETILE) {
+    const uint32_t k0 = c * 16u;
+    if (k0 >= pad && k0 + 16u <= span) {
+      *reinterpret_cast<uint4*>(g0 + k0) = s_buf[c];
+    } else {
+      for (uint32_t k = max(k0, pad); k < min(k0 + 16u, span); ++k) g0[k] = buf[k];
+    }
   }
 }
 
@@ -155,13 +258,8 @@ struct In {
   }
 };
 
-__global__ void decode_kernel(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ offs, uint64_t n,
-                              uint32_t type, pxb_msg* __restrict__ msgs, uint32_t* __restrict__ status) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t b = offs[i], e = offs[i + 1];
-  In r{bytes + b, bytes + (e >= b ? e : b), 0u};
-  pxb_msg m{0, 0, 0, 0};
+__device__ __forceinline__ uint32_t decode_record(In& r, uint32_t type, pxb_msg& m) {
+  m = pxb_msg{0, 0, 0, 0};
   const uint32_t tag = r.u8();
   if (!r.err) {
     if (tag > 2u) {
@@ -187,8 +285,54 @@ __global__ void decode_kernel(const uint8_t* __restrict__ bytes, const uint64_t*
   if (!r.err && r.p != r.end) r.err = PXB_WIRE_E_LENGTH;   // trailing bytes
   m.kind = tag;
   if (r.err) m = pxb_msg{0, 0, 0, 0};
+  return r.err;
+}
+
+// One tile: when its offsets are monotone and its byte range fits the stage,
+// the range is loaded with aligned 16-B loads into LDS and each record parsed
+// from there; any record outside that range (or a tile with malformed
+// offsets) is parsed straight from HBM.
+__global__ __launch_bounds__(DTILE) void decode_kernel(const uint8_t* __restrict__ bytes,
+                                                      const uint64_t* __restrict__ offs, uint64_t n, uint32_t type,
+                                                      pxb_msg* __restrict__ msgs, uint32_t* __restrict__ status) {
+  __shared__ uint4 s_buf[Stage<DTILE>::n];
+  const uint8_t* buf = reinterpret_cast<const uint8_t*>(s_buf);
+  const uint64_t first = (uint64_t)blockIdx.x * DTILE;
+  const uint64_t last = min(first + (uint64_t)DTILE, n);
+  const uint64_t lo = offs[first], hi = offs[last];
+  const bool staged = hi >= lo && hi - lo <= (uint64_t)DTILE * PXB_WIRE_MAX_BYTES;
+  const uint8_t* gsrc = bytes + lo;
+  const uint32_t pad = (uint32_t)((uintptr_t)gsrc & 15u);   // LDS byte k <-> global gsrc - pad + k
+  if (staged) {
+    const uint32_t span = pad + (uint32_t)(hi - lo);
+    const uint8_t* g0 = gsrc - pad;
+    for (uint32_t c = threadIdx.x; c * 16u < span; c += DTILE) {
+      const uint32_t k0 = c * 16u;
+      if (k0 >= pad && k0 + 16u <= span) {
+        s_buf[c] = *reinterpret_cast<const uint4*>(g0 + k0);
+      } else {
+        uint8_t* d = reinterpret_cast<uint8_t*>(s_buf);
+        for (uint32_t k = max(k0, pad); k < min(k0 + 16u, span); ++k) d[k] = g0[k];
+      }
+    }
+  }
+  __syncthreads();
+  const uint64_t i = first + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t b = offs[i], e = offs[i + 1];
+  const uint64_t ee = (e >= b) ? e : b;
+  pxb_msg m;
+  uint32_t err;
+  if (staged && b >= lo && ee <= hi) {
+    const uint8_t* p = buf + pad + (uint32_t)(b - lo);
+    In r{p, p + (uint32_t)(ee - b), 0u};
+    err = decode_record(r, type, m);
+  } else {
+    In r{bytes + b, bytes + ee, 0u};
+    err = decode_record(r, type, m);
+  }
   msgs[i] = m;
-  if (status) status[i] = r.err;
+  if (status) status[i] = err;
 }
 
 // scan scratch (grown on demand, one buffer per device)
@@ -198,7 +342,19 @@ size_t g_tmp_bytes[64];
 
 int hip_fail(hipError_t e) { return (e == hipErrorOutOfMemory) ? PXB_E_OOM : PXB_E_HIP; }
 
-unsigned grid_of(uint64_t n) { return (unsigned)((n + 255) / 256); }
+unsigned tiles_of(uint64_t n, int tile) { return (unsigned)((n + tile - 1) / tile); }
+
+// per-device scratch (grown on demand)
+int scratch(int dev, size_t need) {
+  if (need <= g_tmp_bytes[dev]) return PXB_OK;
+  if (g_tmp[dev]) (void)hipFree(g_tmp[dev]);
+  g_tmp[dev] = nullptr;
+  g_tmp_bytes[dev] = 0;
+  hipError_t e = hipMalloc(&g_tmp[dev], need);
+  if (e != hipSuccess) return hip_fail(e);
+  g_tmp_bytes[dev] = need;
+  return PXB_OK;
+}
 
 }  // namespace pxw
 
@@ -209,27 +365,20 @@ extern "C" {
 int pxb_wire_size(const pxb_msg* d_msgs, uint64_t count, uint32_t type, uint64_t* d_offsets, void* stream) {
   if (type > PXB_WIRE_RESPONSE || !d_offsets || (count && !d_msgs) || count > (1ull << 40)) return PXB_E_INVAL;
   const hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(size_kernel, dim3(grid_of(count ? count : 1)), dim3(256), 0, st, d_msgs, count, type,
-                     d_offsets);
-  if (hipGetLastError() != hipSuccess) return PXB_E_HIP;
+  if (hipMemsetAsync(d_offsets, 0, sizeof(uint64_t), st) != hipSuccess) return PXB_E_HIP;
   if (count == 0) return PXB_OK;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return PXB_E_NODEV;
+  // offsets[1..count] = inclusive sum of the record sizes, computed as the
+  // scan reads the messages
+  hipcub::TransformInputIterator<uint64_t, SizeOp, const pxb_msg*> sizes(d_msgs, SizeOp{type});
   std::lock_guard<std::mutex> lk(g_mu);
   size_t need = 0;
-  if (hipcub::DeviceScan::InclusiveSum(nullptr, need, d_offsets + 1, d_offsets + 1, (int64_t)count, st) !=
-      hipSuccess)
+  if (hipcub::DeviceScan::InclusiveSum(nullptr, need, sizes, d_offsets + 1, (int64_t)count, st) != hipSuccess)
     return PXB_E_HIP;
-  if (need > g_tmp_bytes[dev]) {
-    if (g_tmp[dev]) (void)hipFree(g_tmp[dev]);
-    g_tmp[dev] = nullptr;
-    g_tmp_bytes[dev] = 0;
-    hipError_t e = hipMalloc(&g_tmp[dev], need);
-    if (e != hipSuccess) return hip_fail(e);
-    g_tmp_bytes[dev] = need;
-  }
+  if (int rc = scratch(dev, need)) return rc;
   size_t have = g_tmp_bytes[dev];
-  hipError_t e = hipcub::DeviceScan::InclusiveSum(g_tmp[dev], have, d_offsets + 1, d_offsets + 1, (int64_t)count, st);
+  hipError_t e = hipcub::DeviceScan::InclusiveSum(g_tmp[dev], have, sizes, d_offsets + 1, (int64_t)count, st);
   return (e == hipSuccess) ? PXB_OK : hip_fail(e);
 }
 
@@ -238,8 +387,38 @@ int pxb_wire_encode(const pxb_msg* d_msgs, uint64_t count, uint32_t type, const 
   if (type > PXB_WIRE_RESPONSE || count > (1ull << 40)) return PXB_E_INVAL;
   if (count == 0) return PXB_OK;
   if (!d_msgs || !d_offsets || !d_bytes) return PXB_E_INVAL;
-  hipLaunchKernelGGL(encode_kernel, dim3(grid_of(count)), dim3(256), 0, (hipStream_t)stream, d_msgs, count, type,
-                     d_offsets, d_bytes);
+  hipLaunchKernelGGL(encode_kernel<false>, dim3(tiles_of(count, ETILE)), dim3(ETILE), 0, (hipStream_t)stream, d_msgs,
+                     count, type, const_cast<uint64_t*>(d_offsets), nullptr, d_bytes);
+  return (hipGetLastError() == hipSuccess) ? PXB_OK : PXB_E_HIP;
+}
+
+int pxb_wire_encode_all(const pxb_msg* d_msgs, uint64_t count, uint32_t type, uint64_t* d_offsets,
+                        uint8_t* d_bytes, void* stream) {
+  if (type > PXB_WIRE_RESPONSE || !d_offsets || count > (1ull << 40)) return PXB_E_INVAL;
+  const hipStream_t st = (hipStream_t)stream;
+  if (count == 0) return (hipMemsetAsync(d_offsets, 0, sizeof(uint64_t), st) == hipSuccess) ? PXB_OK : PXB_E_HIP;
+  if (!d_msgs || !d_bytes) return PXB_E_INVAL;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return PXB_E_NODEV;
+  const uint64_t tiles = tiles_of(count, ETILE);
+  std::lock_guard<std::mutex> lk(g_mu);
+  size_t need = 0;
+  if (hipcub::DeviceScan::ExclusiveSum(nullptr, need, (uint64_t*)nullptr, (uint64_t*)nullptr, (int64_t)tiles, st) !=
+      hipSuccess)
+    return PXB_E_HIP;
+  const size_t arr = ((tiles * sizeof(uint64_t)) + 255) & ~(size_t)255;
+  if (int rc = scratch(dev, 2 * arr + need)) return rc;
+  uint64_t* tsum = reinterpret_cast<uint64_t*>(g_tmp[dev]);
+  uint64_t* toff = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(g_tmp[dev]) + arr);
+  void* tmp = reinterpret_cast<char*>(g_tmp[dev]) + 2 * arr;
+  hipLaunchKernelGGL(tile_sum_kernel, dim3((unsigned)((tiles + SUM_TILES - 1) / SUM_TILES)), dim3(ETILE), 0, st, d_msgs,
+                     count, type, tiles, tsum);
+  if (hipGetLastError() != hipSuccess) return PXB_E_HIP;
+  size_t have = need;
+  hipError_t e = hipcub::DeviceScan::ExclusiveSum(tmp, have, tsum, toff, (int64_t)tiles, st);
+  if (e != hipSuccess) return hip_fail(e);
+  hipLaunchKernelGGL(encode_kernel<true>, dim3((unsigned)tiles), dim3(ETILE), 0, st, d_msgs, count, type, d_offsets,
+                     toff, d_bytes);
   return (hipGetLastError() == hipSuccess) ? PXB_OK : PXB_E_HIP;
 }
 
@@ -248,7 +427,7 @@ int pxb_wire_decode(const uint8_t* d_bytes, const uint64_t* d_offsets, uint64_t 
   if (type > PXB_WIRE_RESPONSE || count > (1ull << 40)) return PXB_E_INVAL;
   if (count == 0) return PXB_OK;
   if (!d_offsets || !d_msgs || !d_bytes) return PXB_E_INVAL;
-  hipLaunchKernelGGL(decode_kernel, dim3(grid_of(count)), dim3(256), 0, (hipStream_t)stream, d_bytes, d_offsets,
+  hipLaunchKernelGGL(decode_kernel, dim3(tiles_of(count, DTILE)), dim3(DTILE), 0, (hipStream_t)stream, d_bytes, d_offsets,
                      count, type, d_msgs, d_status);
   return (hipGetLastError() == hipSuccess) ? PXB_OK : PXB_E_HIP;
 }
@@ -287,7 +466,8 @@ int pxb_wire_decode_host(const uint8_t* in, const uint64_t* offsets, uint64_t co
   if (count == 0) return PXB_OK;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return PXB_E_NODEV;
-  const uint64_t nb = offsets[count];
+  uint64_t nb = 0;                                       // bytes the offsets can reach
+  for (uint64_t k = 0; k <= count; ++k) nb = (offsets[k] > nb) ? offsets[k] : nb;
   pxb_msg* d_m = nullptr;
   uint64_t* d_o = nullptr;
   uint8_t* d_b = nullptr;

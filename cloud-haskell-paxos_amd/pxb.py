@@ -191,6 +191,7 @@ def load(path: str = LIB_PATH):
     lib.pxb_canonical_bytes_nofault.restype = C.c_uint64
     for name, args in (("pxb_wire_size", [vp, C.c_uint64, C.c_uint32, vp, vp]),
                        ("pxb_wire_encode", [vp, C.c_uint64, C.c_uint32, vp, vp, vp]),
+                       ("pxb_wire_encode_all", [vp, C.c_uint64, C.c_uint32, vp, vp, vp]),
                        ("pxb_wire_decode", [vp, vp, C.c_uint64, C.c_uint32, vp, vp, vp]),
                        ("pxb_wire_encode_host", [vp, C.c_uint64, C.c_uint32, vp, vp, vp]),
                        ("pxb_wire_decode_host", [vp, vp, C.c_uint64, C.c_uint32, vp, vp])):
@@ -301,6 +302,17 @@ def wire_encode(msgs, wire_type):
     nb = C.c_uint64(0)
     check(lib.pxb_wire_encode_host(_ptr(msgs), n, wire_type, _ptr(out), _ptr(offs), C.byref(nb)))
     return out[:nb.value].tobytes(), offs
+
+
+def wire_encode_device(d_msgs, wire_type, d_offsets, d_bytes, stream=None):
+    """Fused size + encode on device tensors (pxb_wire_encode_all): d_msgs
+    int32 (n, 4), d_offsets int64 (n + 1), d_bytes uint8 (n * WIRE_MAX_BYTES),
+    asynchronous on `stream` (a raw hipStream_t handle, default stream if None)."""
+    lib = load()
+    n = d_msgs.shape[0]
+    assert d_offsets.numel() >= n + 1 and d_bytes.numel() >= max(1, n * WIRE_MAX_BYTES)
+    check(lib.pxb_wire_encode_all(C.c_void_p(d_msgs.data_ptr()), n, wire_type, C.c_void_p(d_offsets.data_ptr()),
+                                  C.c_void_p(d_bytes.data_ptr()), C.c_void_p(stream or 0)))
 
 
 def wire_decode(data: bytes, offsets, wire_type):

@@ -209,10 +209,20 @@ int pxb_proposer_handle(pxb_proposer_rec* states, uint32_t n_acceptors,
 #define PXB_WIRE_E_RANGE   4u     /* Int beyond int32, id > 255, t >= 2^24   */
 
 /* DEVICE buffers, asynchronous on `stream`.  pxb_wire_size writes the
- * offsets of `count` encoded messages (d_offsets: count + 1 entries). */
+ * offsets of `count` encoded messages (d_offsets: count + 1 entries);
+ * pxb_wire_encode takes exactly those offsets (it writes the records of each
+ * message tile contiguously from the tile's first offset).  Decode
+ * accepts any offsets within the buffer: a record with off[i+1] < off[i] is
+ * empty (PXB_WIRE_E_LENGTH). */
 int pxb_wire_size(const pxb_msg* d_msgs, uint64_t count, uint32_t type, uint64_t* d_offsets, void* stream);
 int pxb_wire_encode(const pxb_msg* d_msgs, uint64_t count, uint32_t type, const uint64_t* d_offsets,
                     uint8_t* d_bytes, void* stream);
+/* size + encode fused: writes the offsets (count + 1 entries) and the records;
+ * d_bytes must hold count * PXB_WIRE_MAX_BYTES bytes (or the encoded total).
+ * The size / encode_all calls of one device share a scratch buffer: issue
+ * them on one stream. */
+int pxb_wire_encode_all(const pxb_msg* d_msgs, uint64_t count, uint32_t type, uint64_t* d_offsets,
+                        uint8_t* d_bytes, void* stream);
 /* d_status (nullable): PXB_WIRE_* per message; failed messages decode to 0s */
 int pxb_wire_decode(const uint8_t* d_bytes, const uint64_t* d_offsets, uint64_t count, uint32_t type,
                     pxb_msg* d_msgs, uint32_t* d_status, void* stream);

@@ -140,3 +140,47 @@ def test_gpu_decode_malformed_matches_oracle(gpu_lib, kind):
 def test_gpu_wire_empty_batch(gpu_lib):
     data, offs = pxb.wire_encode(np.zeros((0, 4), np.uint32), W.REQUEST)
     assert data == b"" and list(offs) == [0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", [W.REQUEST, W.RESPONSE])
+def test_gpu_decode_irregular_offsets_matches_oracle(gpu_lib, kind):
+    """Offsets that are not a clean framing: decreasing pairs (an empty record),
+    a tile whose range runs backwards, a tile whose range exceeds the LDS stage.
+    Every record i is bytes[offs[i]:max(offs[i], offs[i+1])], as in the oracle;
+    such tiles are parsed from HBM instead of the LDS stage."""
+    rng = np.random.default_rng(21 + kind)
+    msgs = _batch(kind, 5000, 17 + kind)
+    data, offs = pxb.wire_encode(msgs, kind)
+    offs = np.array(offs, dtype=np.uint64)
+    total = int(offs[-1])
+    for i in rng.choice(np.arange(1, 5000), 40, replace=False):
+        offs[i] = int(rng.integers(0, total + 1))       # random framing errors
+    offs[1024] = total                                   # tile 0 too long, tile 1 backwards
+    offs[3000] = 0
+    got, st = pxb.wire_decode(data, offs, kind)
+    for i in range(5000):
+        b, e = int(offs[i]), int(offs[i + 1])
+        ws, wm = W.decode(data[b:max(b, e)], kind)
+        assert st[i] == ws, (i, b, e, st[i], ws)
+        if ws == W.OK:
+            assert _as_msg(got[i]) == wm
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", [W.REQUEST, W.RESPONSE])
+@pytest.mark.parametrize("n", [1, 255, 256, 257, 20000])
+def test_gpu_encode_all_matches_oracle(gpu_lib, kind, n):
+    """pxb_wire_encode_all (fused size + encode, device buffers) == the oracle,
+    including ragged last tiles."""
+    import torch
+    msgs = _batch(kind, n, 31 + kind + n)
+    d_m = torch.from_numpy(msgs.view(np.int32)).cuda()
+    d_o = torch.full((n + 1,), -1, dtype=torch.int64, device="cuda")
+    d_b = torch.zeros(n * pxb.WIRE_MAX_BYTES, dtype=torch.uint8, device="cuda")
+    pxb.wire_encode_device(d_m, kind, d_o, d_b)
+    torch.cuda.synchronize()
+    offs = d_o.cpu().numpy().astype(np.uint64)
+    want, woffs = W.encode_batch([_as_msg(m) for m in msgs], kind)
+    assert list(offs) == woffs
+    assert d_b[:len(want)].cpu().numpy().tobytes() == want

@@ -11,7 +11,7 @@ import torch  # noqa
 import pxb  # noqa
 
 NAMES = ["refill", "acceptor", "prop_tick+count", "prop_fast", "prop_multi", "endstep", "finish", "exit"]
-CNAMES = ["wave-steps", "acc-iters", "fast-rounds", "multi-calls", "multi-rounds", "philox-sites", "done-blocks", "active-slots"]
+CNAMES = ["wave-steps", "acc-iters", "fast-rounds", "multi-calls", "multi-rounds", "philox-sites", "max-slot-rounds", "active-slots"]
 lib = pxb.load()
 lib.pxb_debug_stamps.argtypes = [C.c_void_p]
 for c, n in ((2, 1 << 20), (3, 1 << 22), (4, 1 << 22), (5, 1 << 20)):
