@@ -242,3 +242,31 @@ def test_host_driver_binary(gpu_lib):
     assert out.returncode == 0, out.stderr
     assert "decided c1.1 @ Ticket 1, rounds 1, steps 6, flags -" in out.stdout
     assert "decided          1024" in out.stdout
+
+
+def _random_config(rng, i):
+    """A schedule drawn from the whole validated parameter space."""
+    log = rng.random() < 0.3
+    return pxb.Config(
+        seed=int(rng.integers(0, 1 << 63)), n_proposers=int(rng.integers(1, 4)),
+        n_acceptors=int(rng.integers(2, 10)),
+        loss_ppm=int(rng.choice([0, 0, rng.integers(1, 600000), 1000000])),
+        delay_max=int(rng.choice([1, 1, rng.integers(2, 16)])),
+        crash_ppm=int(rng.choice([0, rng.integers(1, 1000001)])),
+        crash_len_max=int(rng.integers(1, 40)), crash_start_max=int(rng.integers(0, 30)),
+        skew_max=int(rng.choice([0, rng.integers(1, 12)])),
+        step_cap=int(rng.choice([int(rng.integers(1, 64)), 256, 1024])),
+        randomize=bool(rng.random() < 0.25),
+        n_ticks=int(rng.integers(2, 9)) if log else 1,
+        tick_period=int(rng.integers(1, 21)) if log else 1)
+
+
+@pytest.mark.parametrize("i", range(48))
+def test_random_schedules_match_oracle(gpu_lib, i):
+    """48 seeded draws over every knob (proposers, acceptors, loss, delay, crash
+    windows, skew, step cap, per-instance fuzzing, log mode): results,
+    digests, acceptor records and totals (canonical bytes included) equal the
+    oracle's."""
+    rng = np.random.default_rng(0xF022 + i)
+    cfg = _random_config(rng, i)
+    _cmp(cfg, int(rng.integers(0, 1 << 34)), int(rng.integers(1, 1500)))
