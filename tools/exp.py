@@ -1,7 +1,7 @@
 """A/B timing of library variants (diagnostic; never the bench number).
     python tools/exp.py lib1.so [lib2.so ...]
 For each lib: kernel ms per launch (HIP events on the launch stream) for
-config 2 (2^20, with and without outputs), configs 3 and 4 (2^22) and config 5 (2^20)."""
+config 2 (2^20, with and without outputs), configs 3 and 4 (2^22) config 5 (2^20) and config 6 (log mode, 2^20)."""
 import os
 import sys
 
@@ -47,6 +47,8 @@ def main():
         ms, t = timeit(pxb.CONFIGS[5], 1 << 20, True, 2, 0)
         row.append("c5 %.2f ms (%.1f Minst/s, %.1f ps/inst-step, %.1f ps/msg)" % (
             ms, (1 << 20) / ms / 1e3, ms * 1e9 * 3 / t[12], ms * 1e9 * 3 / t[7]))
+        ms, t = timeit(pxb.CONFIGS[6], 1 << 20, True, 5, 0)
+        row.append("c6 %.3f ms (%.1f Minst/s)" % (ms, (1 << 20) / ms / 1e3))
         print("%-28s %s" % (lib, " | ".join(row)), flush=True)
 
 
