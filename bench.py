@@ -180,9 +180,16 @@ def cpu_baseline(cfg, budget_s):
         if time.perf_counter() - t0 >= budget_s:
             break
     dt = time.perf_counter() - t0
+    # the same port on one core (all host cores and 1 core)
+    one, t1 = 0, time.perf_counter()
+    while time.perf_counter() - t1 < min(3.0, budget_s):
+        oracle_c.run_cpu(cfg, first + done + one, 1 << 14, threads=1)
+        one += 1 << 14
+    dt1 = time.perf_counter() - t1
     return {"value": done / dt, "unit": "instances/s", "cores": threads, "kind": "port",
             "sample": "%d instances of the same config (ids from 2^40), oracle/paxos_oracle.c "
-                      "on %d host threads, %.1f s" % (done, threads, dt)}
+                      "on %d host threads, %.1f s" % (done, threads, dt),
+            "one_core": {"value": one / dt1, "sample": "%d further instances, 1 thread, %.1f s" % (one, dt1)}}
 
 
 def main():
