@@ -110,6 +110,13 @@ static unsigned long long* g_dbg = nullptr;
 static std::mutex g_mu;
 static int g_occ[4][4][10][64];         // [logm*2+ff][pm][n][device] blocks per CU (0 = unknown)
 static int g_cus[64];
+// Work-queue counters of the faulty kernels: QSLOTS pairs per device, 128 B
+// apart.  Each launch takes the next pair round-robin; the kernel's last wave
+// resets its pair to zero, so consecutive launches need no memset.  Up to
+// QSLOTS launches of one device may be in flight at once (on any streams).
+constexpr int QSLOTS = 64, QSTRIDE = 32;
+static uint32_t* g_queue[64];
+static uint32_t g_qseq[64];
 
 static int hip_fail(hipError_t e) {
   g_last_hip = (int)e;
@@ -209,6 +216,13 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
                                                                                           : Occ<3>::waves);
     occ = std::min(o, target);
     cus = g_cus[dev];
+    if (!ff && !g_queue[dev]) {
+      uint32_t* q = nullptr;
+      HIPCHK(hipMalloc(&q, QSLOTS * QSTRIDE * sizeof(uint32_t)));
+      HIPCHK(hipMemset(q, 0, QSLOTS * QSTRIDE * sizeof(uint32_t)));
+      HIPCHK(hipDeviceSynchronize());
+      g_queue[dev] = q;
+    }
     static const char* cap_env = getenv("PXB_BLOCKS_PER_CU");   // experiments: cap residency
     if (cap_env && atoi(cap_env) > 0) occ = std::min(occ, atoi(cap_env));
   }
@@ -245,7 +259,8 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
   const uint64_t G = 64 / cfg->n_acceptors;
   const uint64_t resident = (uint64_t)occ * (uint64_t)cus;
   // a launch must not give any slot 65536 instances (16-bit packed run totals)
-  const uint64_t chunk_max = std::min<uint64_t>(1ull << 31, resident * WPB * G * 60000ull);
+  // (static split), and epoch tags (idx + 1 under the work queue) stay below 2^30
+  const uint64_t chunk_max = std::min<uint64_t>(ff ? (1ull << 31) : (1ull << 30) - 1, resident * WPB * G * 60000ull);
   for (uint64_t done = 0; done < cfg->n_instances; done += chunk_max) {
     const uint64_t nc = std::min<uint64_t>(chunk_max, cfg->n_instances - done);
     kp.first_instance = cfg->first_instance + done;
@@ -253,6 +268,10 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
     kp.out = d_out ? reinterpret_cast<uint4*>(d_out + done) : nullptr;
     kp.dig = d_log_digest ? d_log_digest + done * cfg->n_acceptors : nullptr;
     kp.acc = d_acc ? reinterpret_cast<uint4*>(d_acc + done * cfg->n_acceptors) : nullptr;
+    if (!ff) {
+      std::lock_guard<std::mutex> lk(g_mu);
+      kp.queue = g_queue[dev] + (size_t)(g_qseq[dev]++ % QSLOTS) * QSTRIDE;
+    }
     const uint64_t waves_needed = (nc + G - 1) / G;
     const uint64_t blocks_needed = (waves_needed + WPB - 1) / WPB;
     const unsigned grid = (unsigned)std::min<uint64_t>(blocks_needed, resident);

@@ -60,6 +60,16 @@ constexpr int BLOCK = 64 * WPB;
 #ifndef PXB_OCC_P3
 #define PXB_OCC_P3 2
 #endif
+// Faulty kernels hand out instances from a device work queue in chunks of
+// QCHUNK (instance lengths vary from a few steps to step_cap, so a static
+// split leaves the slowest waves running alone at the end).
+#ifndef PXB_QCHUNK
+#define PXB_QCHUNK 64
+#endif
+constexpr uint32_t QCHUNK = PXB_QCHUNK;
+// a wave flushes its packed 16-bit run totals after taking this many
+// instances from the queue (a slot finishes at most that + QCHUNK + G since)
+constexpr uint32_t FLUSH_EVERY = 30000;
 
 // kp.cfg bit layout
 constexpr uint32_t CFG_RANDOMIZE = 1u << 0;
@@ -80,6 +90,7 @@ struct KParams {
   uint32_t* dig;
   uint4* acc;
   unsigned long long* totals;
+  uint32_t* queue;                    // faulty kernels: {next instance, waves exited}, 0 on entry
   unsigned long long* dbg;            // diagnostic builds only (PXB_STAMPS)
 };
 
@@ -243,9 +254,20 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
   const uint32_t wave = blockIdx.x * WPB + wib;
   const uint32_t nwaves = gridDim.x * WPB;
   const uint32_t n = kp.n_instances;
-  uint32_t next = (uint32_t)((uint64_t)n * wave / nwaves);
+  // fault-free kernels: a static contiguous slice per wave (every instance
+  // takes the same few steps); faulty kernels: chunks from the work queue
+#ifdef PXB_STATIC_SPLIT
+  constexpr bool DYN = false;
+#else
+  constexpr bool DYN = !FF;
+#endif
+  uint32_t next = DYN ? 0u : (uint32_t)((uint64_t)n * wave / nwaves);
+  uint32_t end = DYN ? 0u : (uint32_t)((uint64_t)n * (wave + 1) / nwaves);
+  // epoch tags of the canonical log (idx - first_idx + 1) must grow along a
+  // slot's instances: the queue hands out chunks in increasing order
   const uint32_t first_idx = next;
-  const uint32_t end = (uint32_t)((uint64_t)n * (wave + 1) / nwaves);
+  bool drained = false;                   // DYN: the queue is empty (wave-uniform)
+  uint32_t grabbed = 0;                   // DYN: instances taken since the last flush (wave-uniform)
   const uint32_t k0 = kp.k0, k1 = kp.k1;
 
   // ---- slot state (replicated in the slot's lanes unless marked "lane") ----
@@ -284,6 +306,53 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
     R[p] = Link{0, 0, 0};
     Sx[p] = Link{0, 0, 0};
   }
+
+  // ---- run totals: wave reduction + one atomic per counter, counters zeroed
+  auto flush_totals = [&]() {
+    uint32_t v[14] = {ca & 0xFFFFu, ca >> 16, cb & 0xFFFFu, cb >> 16, cc & 0xFFFFu, cc >> 16,
+                      cd & 0xFFFFu, cd >> 16, ce, rounds_acc, steps_acc, msgs_acc, execs_acc, 0u};
+    uint64_t c64 = canon_acc;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+#pragma unroll
+      for (int q = 0; q < 13; ++q) v[q] += (uint32_t)__shfl_xor((int)v[q], off);
+      const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)c64, off);
+      const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(c64 >> 32), off);
+      c64 += ((uint64_t)hi << 32) | lo;
+    }
+    if (lane < 14) {
+      // lane q adds counter q (one atomic per lane, no serialisation within the wave)
+      const int slot_of[14] = {PXB_C_INSTANCES, PXB_C_UNDECIDED, PXB_C_STUCK, PXB_C_PANIC, PXB_C_DIVERGENCE,
+                               PXB_C_STEP_CAP, PXB_C_QUEUE_OVERFLOW, PXB_C_TICKET_OVERFLOW, PXB_C_LOG_TRUNC,
+                               PXB_C_ROUNDS, PXB_C_STEPS, PXB_C_MESSAGES, PXB_C_EXECUTES, PXB_C_DECIDED};
+      unsigned long long val = 0;
+#pragma unroll
+      for (int q = 0; q < 13; ++q) val = (lane == q) ? (unsigned long long)v[q] : val;
+      if (lane == 13) val = (unsigned long long)v[0] - (unsigned long long)v[1];   // decided
+      if (val) atomicAdd(&kp.totals[slot_of[lane]], val);
+    }
+    if (lane == 14) atomicAdd(&kp.totals[PXB_C_CANON_BYTES], (unsigned long long)c64);
+    ca = cb = cc = cd = ce = rounds_acc = steps_acc = msgs_acc = execs_acc = 0u;
+    canon_acc = 0ull;
+  };
+
+  // rare in-loop variant (every FLUSH_EVERY started instances): each lane adds
+  // its own counts, no wave reduction (keeps register pressure off the loop)
+  auto flush_lanes = [&]() {
+    auto add = [&](int c, uint32_t v) {
+      if (v) atomicAdd(&kp.totals[c], (unsigned long long)v);
+    };
+    add(PXB_C_INSTANCES, ca & 0xFFFFu);
+    add(PXB_C_UNDECIDED, ca >> 16);
+    add(PXB_C_DECIDED, (ca & 0xFFFFu) - (ca >> 16));
+    add(PXB_C_STUCK, cb & 0xFFFFu);
+    add(PXB_C_PANIC, cb >> 16);
+    add(PXB_C_DIVERGENCE, cc & 0xFFFFu);
+    add(PXB_C_STEP_CAP, cc >> 16);
+    add(PXB_C_QUEUE_OVERFLOW, cd & 0xFFFFu);
+    add(PXB_C_TICKET_OVERFLOW, cd >> 16);
+    ca = cb = cc = cd = 0u;
+  };
 
   STAMP_DECL
   // common link send, predicated on `pred` (docs/SEMANTICS.md §5): Philox
@@ -384,6 +453,19 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
   for (;;) {
     // ---------------- refill free slots from this wave's range -------------
     const uint64_t freeb = ballot(used && !active && a == 0);
+    if (DYN && freeb != 0ull && next >= end && !drained) {
+      uint32_t c = 0u;
+      if (lane == 0) c = atomicAdd(&kp.queue[0], QCHUNK);
+      c = (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
+      drained = c >= n;
+      next = drained ? next : c;
+      end = drained ? end : min(c + QCHUNK, n);
+      grabbed += QCHUNK;
+      if (grabbed >= FLUSH_EVERY) {   // keep the 16-bit slot counts below 2^16
+        flush_lanes();
+        grabbed = 0;
+      }
+    }
     if (freeb != 0ull && next < end) {
       const uint32_t cand = next + (uint32_t)__popcll(freeb & ((1ull << base) - 1ull));
       if (used && !active && cand < end) {
@@ -885,30 +967,17 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
 
   STAMP(7);
   STAMP_FLUSH(kp.dbg);
-  // ---------------- flush lane totals -----------------------------------------
-  uint32_t v[14] = {ca & 0xFFFFu, ca >> 16, cb & 0xFFFFu, cb >> 16, cc & 0xFFFFu, cc >> 16,
-                    cd & 0xFFFFu, cd >> 16, ce, rounds_acc, steps_acc, msgs_acc, execs_acc, 0u};
-  uint64_t c64 = canon_acc;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-#pragma unroll
-    for (int q = 0; q < 13; ++q) v[q] += (uint32_t)__shfl_xor((int)v[q], off);
-    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)c64, off);
-    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(c64 >> 32), off);
-    c64 += ((uint64_t)hi << 32) | lo;
+  flush_totals();
+  if constexpr (DYN) {
+    // the last wave out resets the queue for the next launch that uses it
+    if (lane == 0) {
+      __threadfence();
+      if (atomicAdd(&kp.queue[1], 1u) == nwaves - 1u) {
+        atomicExch(&kp.queue[0], 0u);
+        atomicExch(&kp.queue[1], 0u);
+      }
+    }
   }
-  if (lane < 14) {
-    // lane q adds counter q (one atomic per lane, no serialisation within the wave)
-    const int slot_of[14] = {PXB_C_INSTANCES, PXB_C_UNDECIDED, PXB_C_STUCK, PXB_C_PANIC, PXB_C_DIVERGENCE,
-                             PXB_C_STEP_CAP, PXB_C_QUEUE_OVERFLOW, PXB_C_TICKET_OVERFLOW, PXB_C_LOG_TRUNC,
-                             PXB_C_ROUNDS, PXB_C_STEPS, PXB_C_MESSAGES, PXB_C_EXECUTES, PXB_C_DECIDED};
-    unsigned long long val = 0;
-#pragma unroll
-    for (int q = 0; q < 13; ++q) val = (lane == q) ? (unsigned long long)v[q] : val;
-    if (lane == 13) val = (unsigned long long)v[0] - (unsigned long long)v[1];   // decided
-    if (val) atomicAdd(&kp.totals[slot_of[lane]], val);
-  }
-  if (lane == 14) atomicAdd(&kp.totals[PXB_C_CANON_BYTES], (unsigned long long)c64);
 }
 
 }  // namespace pxb
