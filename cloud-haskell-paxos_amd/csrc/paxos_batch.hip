@@ -223,7 +223,7 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
       HIPCHK(hipDeviceSynchronize());
       g_queue[dev] = q;
     }
-    static const char* cap_env = getenv("PXB_BLOCKS_PER_CU");   // experiments: cap residency
+    const char* cap_env = getenv("PXB_BLOCKS_PER_CU");   // tests / experiments: cap residency
     if (cap_env && atoi(cap_env) > 0) occ = std::min(occ, atoi(cap_env));
   }
   KParams kp;

@@ -62,9 +62,12 @@ constexpr int BLOCK = 64 * WPB;
 #endif
 // Faulty kernels hand out instances from a device work queue in chunks of
 // QCHUNK (instance lengths vary from a few steps to step_cap, so a static
-// split leaves the slowest waves running alone at the end).
+// split leaves the slowest waves running alone at the end).  One counter is
+// enough: eight sub-queues with stealing measured no faster, and the
+// fault-free kernels keep their static slices (a queue there costs 4x: every
+// wave would hit the counter every ~12 steps).
 #ifndef PXB_QCHUNK
-#define PXB_QCHUNK 64
+#define PXB_QCHUNK 16   // measured: 8 = 16 > 32 > 64 > 256 on configs 3-5
 #endif
 constexpr uint32_t QCHUNK = PXB_QCHUNK;
 // a wave flushes its packed 16-bit run totals after taking this many

@@ -180,6 +180,48 @@ def test_device_entry_accumulates_totals(gpu_lib):
     assert np.array_equal(out.cpu().numpy().view(np.uint32), eres)
 
 
+def test_work_queue_flush_keeps_totals_exact(gpu_lib):
+    """Faulty kernels take instances from a device work queue and flush their
+    packed 16-bit per-slot counts every FLUSH_EVERY (30000) taken instances.
+    With one wave per CU each wave takes ~65K instances here, so every wave
+    flushes mid-run; the totals must still equal the per-instance results."""
+    cfg = pxb.Config(seed=0xF1, n_proposers=1, n_acceptors=3, delay_max=2, step_cap=64)
+    n = 1 << 24
+    os.environ["PXB_BLOCKS_PER_CU"] = "1"
+    try:
+        res, _, _, cnt = pxb.run(cfg, 5, n, want_digests=False)
+    finally:
+        del os.environ["PXB_BLOCKS_PER_CU"]
+    flags = res[:, 3] & 0xFF
+    assert cnt["instances"] == n
+    assert cnt["decided"] == int((res[:, 0] != 0).sum())
+    assert cnt["undecided"] == int(((flags & pxb.F_UNDECIDED) != 0).sum())
+    assert cnt["step_cap"] == int(((flags & pxb.F_STEP_CAP) != 0).sum())
+    assert cnt["rounds"] == int(res[:, 2].astype(np.int64).sum())
+    assert cnt["steps"] == int((res[:, 3] >> 16).astype(np.int64).sum())
+    rng = np.random.default_rng(5)
+    for i in rng.choice(n, 32, replace=False):
+        eres, _, _, _ = oracle_c.run_cpu(cfg, 5 + int(i), 1)
+        assert np.array_equal(res[i], eres[0])
+
+
+def test_work_queue_many_launches(gpu_lib):
+    """The queue counter pairs are reused round-robin (64 per device) and reset
+    by each launch's last wave: 150 back-to-back launches on one stream must
+    each run their whole batch."""
+    import torch
+    cfg = pxb.CONFIGS[4]
+    n, k = 211, 150
+    tot = torch.zeros(16, dtype=torch.int64, device="cuda")
+    out = torch.zeros((k * n, 4), dtype=torch.int32, device="cuda")
+    for j in range(k):
+        pxb.run_device(cfg, j * n, n, d_results=out[j * n:(j + 1) * n], d_totals=tot)
+    torch.cuda.synchronize()
+    eres, _, _, ecnt = oracle_c.run_cpu(cfg, 0, k * n, threads=THREADS)
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), eres)
+    assert pxb.counters_dict(tot.cpu().tolist()) == ecnt
+
+
 # ---- single-handler hooks: the kernel's device functions vs oracle handlers --
 def test_acceptor_hook_matches_oracle(gpu_lib):
     rng = np.random.default_rng(1)
