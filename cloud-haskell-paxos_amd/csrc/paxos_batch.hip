@@ -66,11 +66,37 @@ __global__ void proposer_hook_kernel(pxb_proposer_rec* st, uint32_t n_acc, const
   nb[i] = no;
 }
 
+// Sums the TCOPIES partial rows into the caller's totals, zeroes them and
+// resets the work queue, so the launch slot is clean for its next use.  One
+// block of TCOPIES threads; thread t reads column t % 16 of rows t/16, t/16+16, ...
+__global__ __launch_bounds__(TCOPIES) void finalize_kernel(unsigned long long* part, uint32_t* queue,
+                                                            unsigned long long* totals) {
+  __shared__ unsigned long long acc[16];
+  const uint32_t t = threadIdx.x;
+  if (t < 16) acc[t] = 0ull;
+  __syncthreads();
+  unsigned long long v = 0ull;
+#pragma unroll
+  for (uint32_t j = 0; j < 16; ++j) {
+    v += part[t + j * TCOPIES];
+    part[t + j * TCOPIES] = 0ull;
+  }
+  if (v) atomicAdd(&acc[t % 16u], v);
+  __syncthreads();
+  if (t < 16 && acc[t]) atomicAdd(&totals[t], acc[t]);
+  if (t == 16 && queue) queue[0] = 0u;
+}
+
 // ---- host side ----------------------------------------------------------------
-typedef void (*kernel_fn)(KParams);
+typedef void (*kernel_ptr)(KParams);
+struct kernel_fn {
+  kernel_ptr fn;
+  int wpb;                       // waves per block (Shape<>::wpb)
+  explicit operator bool() const { return fn != nullptr; }
+};
 
 template <int PM, int N, bool LOGM, bool FF>
-static kernel_fn kfn() { return paxos_batch_kernel<PM, N, LOGM, FF>; }
+static kernel_fn kfn() { return kernel_fn{paxos_batch_kernel<PM, N, LOGM, FF>, Shape<PM, N, LOGM, FF>::wpb}; }
 
 template <int PM, bool LOGM, bool FF>
 static kernel_fn pick_n(uint32_t n) {
@@ -84,7 +110,7 @@ static kernel_fn pick_n(uint32_t n) {
     case 8: return kfn<PM, 8, LOGM, FF>();
     case 9: return kfn<PM, 9, LOGM, FF>();
   }
-  return nullptr;
+  return kernel_fn{nullptr, 0};
 }
 
 template <int PM>
@@ -100,7 +126,7 @@ static kernel_fn pick(uint32_t pm, uint32_t n, bool logm, bool ff) {
     case 2: return pick_mode<2>(n, logm, ff);
     case 3: return pick_mode<3>(n, logm, ff);
   }
-  return nullptr;
+  return kernel_fn{nullptr, 0};
 }
 
 static thread_local int g_last_hip = 0;
@@ -110,12 +136,14 @@ static unsigned long long* g_dbg = nullptr;
 static std::mutex g_mu;
 static int g_occ[4][4][10][64];         // [logm*2+ff][pm][n][device] blocks per CU (0 = unknown)
 static int g_cus[64];
-// Work-queue counters of the faulty kernels: QSLOTS pairs per device, 128 B
-// apart.  Each launch takes the next pair round-robin; the kernel's last wave
-// resets its pair to zero, so consecutive launches need no memset.  Up to
-// QSLOTS launches of one device may be in flight at once (on any streams).
-constexpr int QSLOTS = 64, QSTRIDE = 32;
-static uint32_t* g_queue[64];
+// Per-launch scratch: QSLOTS slots per device, each TCOPIES partial-total rows
+// (16 x u64) + the work-queue counter on its own 128-B line.  Each launch takes
+// the next slot round-robin; its finalize_kernel leaves the slot zeroed, so
+// consecutive launches need no memset.  Up to QSLOTS launches of one device
+// may be in flight at once (on any streams).
+constexpr int QSLOTS = 64;
+constexpr size_t SLOT_U64 = (size_t)TCOPIES * 16 + 16;
+static unsigned long long* g_slots[64];
 static uint32_t g_qseq[64];
 
 static int hip_fail(hipError_t e) {
@@ -159,6 +187,18 @@ int pxb_debug_stamps(unsigned long long* out16) {
   HIPCHK(hipMemcpy(out16, g_dbg, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
   HIPCHK(hipMemset(g_dbg, 0, 16 * sizeof(unsigned long long)));
   return PXB_OK;
+}
+#endif
+#ifdef PXB_WAVE_TIMES
+// diagnostic build only: (start, end, HW_ID, XCC_ID, shader-clock start, end) of every wave of the last launch
+static unsigned long long* g_wt = nullptr;
+static unsigned g_wt_waves = 0;
+int pxb_debug_wave_times(unsigned long long* out, unsigned max_waves) {
+  if (!g_wt) return PXB_E_INVAL;
+  HIPCHK(hipDeviceSynchronize());
+  const unsigned nw = std::min(g_wt_waves, max_waves);
+  HIPCHK(hipMemcpy(out, g_wt, 6ull * nw * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  return (int)nw;
 }
 #endif
 int pxb_last_hip_error(void) { return g_last_hip; }
@@ -205,23 +245,22 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
     int& o = g_occ[(logm ? 2 : 0) + (ff ? 1 : 0)][cfg->n_proposers][cfg->n_acceptors][dev];
     if (!o) {
       int nb = 0;
-      HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)fn, BLOCK, 0));
+      HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)fn.fn, 64 * fn.wpb, 0));
       o = std::max(1, nb);
     }
     // Residency: the launch-bounds target (waves per SIMD x 4 SIMDs), even when
-    // a small kernel would fit more.  Every wave owns an equal contiguous slice
-    // of the batch, so more waves means fewer, more often partially filled slot
-    // generations per wave (measured: 4 -> 6 waves/SIMD costs 5 % on config 2).
+    // a small kernel would fit more (measured: 4 -> 6 waves/SIMD costs 5 % on
+    // config 2: more, more often partially filled slot generations per wave).
     const int target = 4 * (cfg->n_proposers == 1 ? Occ<1>::waves : cfg->n_proposers == 2 ? Occ<2>::waves
                                                                                           : Occ<3>::waves);
-    occ = std::min(o, target);
+    occ = std::min(o, std::max(1, target / fn.wpb));   // blocks per CU
     cus = g_cus[dev];
-    if (!ff && !g_queue[dev]) {
-      uint32_t* q = nullptr;
-      HIPCHK(hipMalloc(&q, QSLOTS * QSTRIDE * sizeof(uint32_t)));
-      HIPCHK(hipMemset(q, 0, QSLOTS * QSTRIDE * sizeof(uint32_t)));
+    if (!g_slots[dev]) {
+      unsigned long long* q = nullptr;
+      HIPCHK(hipMalloc(&q, QSLOTS * SLOT_U64 * sizeof(unsigned long long)));
+      HIPCHK(hipMemset(q, 0, QSLOTS * SLOT_U64 * sizeof(unsigned long long)));
       HIPCHK(hipDeviceSynchronize());
-      g_queue[dev] = q;
+      g_slots[dev] = q;
     }
     const char* cap_env = getenv("PXB_BLOCKS_PER_CU");   // tests / experiments: cap residency
     if (cap_env && atoi(cap_env) > 0) occ = std::min(occ, atoi(cap_env));
@@ -244,7 +283,7 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
   kp.cfg = ((cfg->flags & PXB_CFG_RANDOMIZE) ? CFG_RANDOMIZE : 0u) | (lt ? CFG_LOSSY : 0u) | (ct ? CFG_CRASHY : 0u);
   kp.loss_m1 = (uint32_t)(lt - 1ull);
   kp.crash_m1 = (uint32_t)(ct - 1ull);
-  kp.totals = reinterpret_cast<unsigned long long*>(d_totals);
+  unsigned long long* const totals = reinterpret_cast<unsigned long long*>(d_totals);
 #ifdef PXB_STAMPS
   {
     static unsigned long long* dbg = nullptr;
@@ -258,9 +297,13 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
 #endif
   const uint64_t G = 64 / cfg->n_acceptors;
   const uint64_t resident = (uint64_t)occ * (uint64_t)cus;
-  // a launch must not give any slot 65536 instances (16-bit packed run totals)
-  // (static split), and epoch tags (idx + 1 under the work queue) stay below 2^30
-  const uint64_t chunk_max = std::min<uint64_t>(ff ? (1ull << 31) : (1ull << 30) - 1, resident * WPB * G * 60000ull);
+  // a launch must not give any slot 65536 instances (16-bit packed run totals):
+  // on average 30000 per slot for the block-queue kernels (uniform instance
+  // lengths), 60000 for the work-queue kernels (which also flush mid-run);
+  // epoch tags (idx + 1 under the work queue) stay below 2^30
+  const uint64_t wpb = (uint64_t)fn.wpb;
+  const uint64_t chunk_max = ff ? std::min<uint64_t>(1ull << 31, resident * wpb * G * 30000ull)
+                                : std::min<uint64_t>((1ull << 30) - 1, resident * wpb * G * 60000ull);
   for (uint64_t done = 0; done < cfg->n_instances; done += chunk_max) {
     const uint64_t nc = std::min<uint64_t>(chunk_max, cfg->n_instances - done);
     kp.first_instance = cfg->first_instance + done;
@@ -268,14 +311,24 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
     kp.out = d_out ? reinterpret_cast<uint4*>(d_out + done) : nullptr;
     kp.dig = d_log_digest ? d_log_digest + done * cfg->n_acceptors : nullptr;
     kp.acc = d_acc ? reinterpret_cast<uint4*>(d_acc + done * cfg->n_acceptors) : nullptr;
-    if (!ff) {
+    {
       std::lock_guard<std::mutex> lk(g_mu);
-      kp.queue = g_queue[dev] + (size_t)(g_qseq[dev]++ % QSLOTS) * QSTRIDE;
+      unsigned long long* slot = g_slots[dev] + (size_t)(g_qseq[dev]++ % QSLOTS) * SLOT_U64;
+      kp.part = slot;
+      kp.queue = reinterpret_cast<uint32_t*>(slot + (size_t)TCOPIES * 16);
     }
     const uint64_t waves_needed = (nc + G - 1) / G;
-    const uint64_t blocks_needed = (waves_needed + WPB - 1) / WPB;
+    const uint64_t blocks_needed = (waves_needed + wpb - 1) / wpb;
     const unsigned grid = (unsigned)std::min<uint64_t>(blocks_needed, resident);
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(BLOCK), 0, st, kp);
+#ifdef PXB_WAVE_TIMES
+    if (!g_wt) HIPCHK(hipMalloc(&g_wt, 6ull * 65536 * sizeof(unsigned long long)));
+    kp.dbg = g_wt;
+    g_wt_waves = grid * fn.wpb;
+    if (grid * fn.wpb > 65536) return PXB_E_INVAL;
+#endif
+    hipLaunchKernelGGL(fn.fn, dim3(grid), dim3(64 * fn.wpb), 0, st, kp);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(TCOPIES), 0, st, kp.part, ff ? nullptr : kp.queue, totals);
     HIPCHK(hipGetLastError());
   }
   return PXB_OK;

@@ -46,11 +46,6 @@ constexpr int QD = PXB_QUEUE_DEPTH;   // 8: ring slots per directed link
 constexpr int LT = PXB_LOG_TRACK;
 static_assert(QD == 8, "due-nibble word and ring masks assume 8 slots");
 static_assert(PXB_MAX_STEP_CAP <= 8192, "14-bit packed tickets / steps");
-#ifndef PXB_WPB
-#define PXB_WPB 1
-#endif
-constexpr int WPB = PXB_WPB;          // waves per block (LDS is carved per wave)
-constexpr int BLOCK = 64 * WPB;
 #ifndef PXB_OCC_P1
 #define PXB_OCC_P1 4
 #endif
@@ -70,6 +65,12 @@ constexpr int BLOCK = 64 * WPB;
 #define PXB_QCHUNK 16   // measured: 8 = 16 > 32 > 64 > 256 on configs 3-5
 #endif
 constexpr uint32_t QCHUNK = PXB_QCHUNK;
+// Run totals: each wave adds its counts into row (wave % TCOPIES) of a
+// partial-totals block, and finalize_kernel (launched right after on the same
+// stream) sums the rows into the caller's totals, zeroes them and resets the
+// queue.  All waves adding into one 128-B row serialise at the L2: 4096 waves
+// x 15 counters cost ~70-100 us per launch, a third of a config-2 launch.
+constexpr uint32_t TCOPIES = 256;
 // a wave flushes its packed 16-bit run totals after taking this many
 // instances from the queue (a slot finishes at most that + QCHUNK + G since)
 constexpr uint32_t FLUSH_EVERY = 30000;
@@ -92,8 +93,8 @@ struct KParams {
   uint4* out;                         // pxb_result records (nullable)
   uint32_t* dig;
   uint4* acc;
-  unsigned long long* totals;
-  uint32_t* queue;                    // faulty kernels: {next instance, waves exited}, 0 on entry
+  unsigned long long* part;           // TCOPIES partial run-total rows (16 counters, 128 B each)
+  uint32_t* queue;                    // faulty kernels: next instance, 0 on entry
   unsigned long long* dbg;            // diagnostic builds only (PXB_STAMPS)
 };
 
@@ -204,6 +205,37 @@ template <int PM> struct Occ { static constexpr int waves = PXB_OCC_P1; };
 template <> struct Occ<2> { static constexpr int waves = PXB_OCC_P2; };
 template <> struct Occ<3> { static constexpr int waves = PXB_OCC_P3; };
 
+// Waves per block (LDS is carved per wave).  Faulty kernels: one wave per
+// block, balanced by the device work queue.  Fault-free kernels: as many of a
+// CU's waves as the LDS allows in one block (16 at 4 waves/SIMD), sharing the
+// block's instance range through an LDS counter.  The SIMD arbiter favours
+// older waves, so with a static slice per wave the waves of a SIMD finish up
+// to 1.5x apart and the SIMD runs its tail with 1-3 waves; a shared range
+// keeps all of them busy until the block's range is done.
+constexpr int LDS_BYTES = 163840;
+template <int PM, int N, bool LOGM, bool FF>
+struct Shape {
+  static constexpr int lds = (int)sizeof(Lds<PM, N, LOGM>);
+  static constexpr int cap = 4 * Occ<PM>::waves;   // waves per CU at the occupancy target
+#ifdef PXB_WPB
+  static constexpr int wpb = PXB_WPB;
+#else
+  // waves resident per CU with w waves per block (LDS- and target-limited)
+  static constexpr int resident(int w) {
+    return (w * lds > LDS_BYTES || w > cap) ? 0 : ((LDS_BYTES / (w * lds)) * w < cap ? (LDS_BYTES / (w * lds)) * w : cap);
+  }
+  // the largest power-of-two block that keeps the most waves resident
+  static constexpr int best() {
+    int b = 1;
+    for (int w = 2; w <= 16; w *= 2)
+      if (resident(w) >= resident(b)) b = w;
+    return b;
+  }
+  static constexpr int wpb = FF ? best() : 1;
+#endif
+  static constexpr int block = 64 * wpb;
+};
+
 // Philox with its inputs made opaque, so the compiler cannot hoist the
 // per-instance half of the rounds (quarter-rate multiplies) out of the rare
 // fault branch into every step.
@@ -226,7 +258,8 @@ __device__ __forceinline__ uint4 philox_here(uint32_t c0, uint32_t c1, uint32_t 
 // count is its length (requests) or its length before this step's acceptor
 // phase (responses), and no Philox draw, due-nibble or isolation test is needed.
 template <int PM, int N, bool LOGM, bool FF>
-__global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KParams kp) {
+__global__ __launch_bounds__((Shape<PM, N, LOGM, FF>::block), Occ<PM>::waves) void paxos_batch_kernel(KParams kp) {
+  constexpr int WPB = Shape<PM, N, LOGM, FF>::wpb;
   constexpr int G = 64 / N;
   constexpr uint32_t NM = (1u << N) - 1u;     // slot-local lane mask
   constexpr uint32_t ENONE = 16u;             // "no event" acceptor index (N <= 9 < 16)
@@ -257,21 +290,34 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
   const uint32_t wave = blockIdx.x * WPB + wib;
   const uint32_t nwaves = gridDim.x * WPB;
   const uint32_t n = kp.n_instances;
-  // fault-free kernels: a static contiguous slice per wave (every instance
-  // takes the same few steps); faulty kernels: chunks from the work queue
+  // faulty kernels: chunks from the device work queue (DYN); fault-free
+  // kernels: one-generation chunks of the block's contiguous range from an
+  // LDS counter (BQ); diagnostic builds: a static slice per wave
 #ifdef PXB_STATIC_SPLIT
-  constexpr bool DYN = false;
+  constexpr bool DYN = false, BQ = false;
 #else
-  constexpr bool DYN = !FF;
+  // (a one-wave block gains nothing from the LDS counter: measured 2 % slower)
+  constexpr bool DYN = !FF, BQ = FF && WPB > 1;
 #endif
-  uint32_t next = DYN ? 0u : (uint32_t)((uint64_t)n * wave / nwaves);
-  uint32_t end = DYN ? 0u : (uint32_t)((uint64_t)n * (wave + 1) / nwaves);
+  __shared__ uint32_t s_bq;
+  const uint32_t blo = (uint32_t)((uint64_t)n * blockIdx.x / gridDim.x);
+  const uint32_t bhi = (uint32_t)((uint64_t)n * (blockIdx.x + 1) / gridDim.x);
+  if constexpr (BQ) {
+    if (threadIdx.x == 0) s_bq = 0u;
+    __syncthreads();
+  }
+  uint32_t next = (DYN || BQ) ? 0u : (uint32_t)((uint64_t)n * wave / nwaves);
+  uint32_t end = (DYN || BQ) ? 0u : (uint32_t)((uint64_t)n * (wave + 1) / nwaves);
   // epoch tags of the canonical log (idx - first_idx + 1) must grow along a
-  // slot's instances: the queue hands out chunks in increasing order
-  const uint32_t first_idx = next;
+  // slot's instances: both queues hand out chunks in increasing order
+  const uint32_t first_idx = BQ ? blo : next;
   bool drained = false;                   // DYN: the queue is empty (wave-uniform)
   uint32_t grabbed = 0;                   // DYN: instances taken since the last flush (wave-uniform)
   const uint32_t k0 = kp.k0, k1 = kp.k1;
+#ifdef PXB_WAVE_TIMES   // diagnostic: per-wave start / end (100 MHz constant clock)
+  const uint64_t wt0 = __builtin_amdgcn_s_memrealtime();
+  const uint64_t wm0 = __builtin_amdgcn_s_memtime();
+#endif
 
   // ---- slot state (replicated in the slot's lanes unless marked "lane") ----
   bool active = false;
@@ -310,6 +356,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
     Sx[p] = Link{0, 0, 0};
   }
 
+  unsigned long long* const trow = kp.part + (size_t)(wave % TCOPIES) * 16u;
   // ---- run totals: wave reduction + one atomic per counter, counters zeroed
   auto flush_totals = [&]() {
     uint32_t v[14] = {ca & 0xFFFFu, ca >> 16, cb & 0xFFFFu, cb >> 16, cc & 0xFFFFu, cc >> 16,
@@ -332,9 +379,13 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
 #pragma unroll
       for (int q = 0; q < 13; ++q) val = (lane == q) ? (unsigned long long)v[q] : val;
       if (lane == 13) val = (unsigned long long)v[0] - (unsigned long long)v[1];   // decided
-      if (val) atomicAdd(&kp.totals[slot_of[lane]], val);
+#ifndef PXB_NO_TOTALS_DIAG   // diagnostic: the cost of the totals atomics
+      if (val) atomicAdd(&trow[slot_of[lane]], val);
+#endif
     }
-    if (lane == 14) atomicAdd(&kp.totals[PXB_C_CANON_BYTES], (unsigned long long)c64);
+#ifndef PXB_NO_TOTALS_DIAG
+    if (lane == 14) atomicAdd(&trow[PXB_C_CANON_BYTES], (unsigned long long)c64);
+#endif
     ca = cb = cc = cd = ce = rounds_acc = steps_acc = msgs_acc = execs_acc = 0u;
     canon_acc = 0ull;
   };
@@ -343,7 +394,7 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
   // its own counts, no wave reduction (keeps register pressure off the loop)
   auto flush_lanes = [&]() {
     auto add = [&](int c, uint32_t v) {
-      if (v) atomicAdd(&kp.totals[c], (unsigned long long)v);
+      if (v) atomicAdd(&trow[c], (unsigned long long)v);
     };
     add(PXB_C_INSTANCES, ca & 0xFFFFu);
     add(PXB_C_UNDECIDED, ca >> 16);
@@ -456,6 +507,14 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
   for (;;) {
     // ---------------- refill free slots from this wave's range -------------
     const uint64_t freeb = ballot(used && !active && a == 0);
+    if (BQ && freeb != 0ull && next >= end && !drained) {
+      uint32_t c = 0u;
+      if (lane == 0) c = atomicAdd(&s_bq, (uint32_t)G);
+      c = (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
+      drained = c >= bhi - blo;
+      next = drained ? next : blo + c;
+      end = drained ? end : min(blo + c + (uint32_t)G, bhi);
+    }
     if (DYN && freeb != 0ull && next >= end && !drained) {
       uint32_t c = 0u;
       if (lane == 0) c = atomicAdd(&kp.queue[0], QCHUNK);
@@ -970,17 +1029,18 @@ __global__ __launch_bounds__(BLOCK, Occ<PM>::waves) void paxos_batch_kernel(KPar
 
   STAMP(7);
   STAMP_FLUSH(kp.dbg);
-  flush_totals();
-  if constexpr (DYN) {
-    // the last wave out resets the queue for the next launch that uses it
-    if (lane == 0) {
-      __threadfence();
-      if (atomicAdd(&kp.queue[1], 1u) == nwaves - 1u) {
-        atomicExch(&kp.queue[0], 0u);
-        atomicExch(&kp.queue[1], 0u);
-      }
-    }
+#ifdef PXB_WAVE_TIMES
+  {
+    const uint64_t wt1 = __builtin_amdgcn_s_memrealtime();
+    const uint64_t wm1 = __builtin_amdgcn_s_memtime();
+    // HW_ID (SIMD, CU, SE fields) and XCC_ID hardware registers
+    const uint64_t hw = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+    const uint64_t xcc = (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 20);
+    if (lane < 6)
+      kp.dbg[6 * wave + lane] = lane == 0 ? wt0 : lane == 1 ? wt1 : lane == 2 ? hw : lane == 3 ? xcc : lane == 4 ? wm0 : wm1;
   }
+#endif
+  flush_totals();
 }
 
 }  // namespace pxb

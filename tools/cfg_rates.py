@@ -13,6 +13,9 @@ if len(sys.argv) > 1:
 CASES = ((2, 1 << 20, 10), (3, 1 << 22, 2), (4, 1 << 23, 2), (4, 1 << 26, 1), (5, 1 << 22, 1), (6, 1 << 20, 3))
 if os.environ.get("PXB_RATES_QUICK"):
     CASES = tuple(c for c in CASES if c[1] <= (1 << 23))
+if os.environ.get("PXB_RATES_CONFIGS"):
+    keep = [int(x) for x in os.environ["PXB_RATES_CONFIGS"].split(",")]
+    CASES = tuple(c for c in CASES if c[0] in keep)
 for c, n, reps in CASES:
     cfg = pxb.CONFIGS[c]
     N = cfg.n_acceptors
