@@ -134,7 +134,12 @@ int pxb_run(const pxb_config* cfg, pxb_result* out, uint32_t* log_digest,
 /* pxb_run_device: DEVICE buffers, asynchronous on `stream` (a hipStream_t;
  * NULL = default stream).  Same outputs as pxb_run but all pointers are device
  * pointers on the current device.  d_totals (PXB_NCOUNTERS int64) is ADDED to,
- * not overwritten, so many launches can accumulate into one vector.         */
+ * not overwritten, so many launches can accumulate into one vector.  Each
+ * call enqueues the batch kernel and a one-block finalize kernel (it folds
+ * the per-launch partial totals into d_totals) per chunk of the batch (2^29
+ * instances at most on faulty schedules), each chunk using one of 64
+ * per-device scratch slots round-robin: at most 64 chunks per device may be
+ * in flight at once across streams.                                        */
 int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_digest,
                    pxb_acceptor_rec* d_acc, int64_t* d_totals, void* stream);
 
