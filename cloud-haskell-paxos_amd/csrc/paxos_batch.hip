@@ -92,11 +92,12 @@ typedef void (*kernel_ptr)(KParams);
 struct kernel_fn {
   kernel_ptr fn;
   int wpb;                       // waves per block (Shape<>::wpb)
+  int occ;                       // waves per SIMD target (Shape<>::occ)
   explicit operator bool() const { return fn != nullptr; }
 };
 
 template <int PM, int N, bool LOGM, bool FF>
-static kernel_fn kfn() { return kernel_fn{paxos_batch_kernel<PM, N, LOGM, FF>, Shape<PM, N, LOGM, FF>::wpb}; }
+static kernel_fn kfn() { return kernel_fn{paxos_batch_kernel<PM, N, LOGM, FF>, Shape<PM, N, LOGM, FF>::wpb, Shape<PM, N, LOGM, FF>::occ}; }
 
 template <int PM, bool LOGM, bool FF>
 static kernel_fn pick_n(uint32_t n) {
@@ -110,7 +111,7 @@ static kernel_fn pick_n(uint32_t n) {
     case 8: return kfn<PM, 8, LOGM, FF>();
     case 9: return kfn<PM, 9, LOGM, FF>();
   }
-  return kernel_fn{nullptr, 0};
+  return kernel_fn{nullptr, 0, 0};
 }
 
 template <int PM>
@@ -126,7 +127,7 @@ static kernel_fn pick(uint32_t pm, uint32_t n, bool logm, bool ff) {
     case 2: return pick_mode<2>(n, logm, ff);
     case 3: return pick_mode<3>(n, logm, ff);
   }
-  return kernel_fn{nullptr, 0};
+  return kernel_fn{nullptr, 0, 0};
 }
 
 static thread_local int g_last_hip = 0;
@@ -251,8 +252,7 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
     // Residency: the launch-bounds target (waves per SIMD x 4 SIMDs), even when
     // a small kernel would fit more (measured: 4 -> 6 waves/SIMD costs 5 % on
     // config 2: more, more often partially filled slot generations per wave).
-    const int target = 4 * (cfg->n_proposers == 1 ? Occ<1>::waves : cfg->n_proposers == 2 ? Occ<2>::waves
-                                                                                          : Occ<3>::waves);
+    const int target = 4 * fn.occ;
     occ = std::min(o, std::max(1, target / fn.wpb));   // blocks per CU
     cus = g_cus[dev];
     if (!g_slots[dev]) {

@@ -49,11 +49,14 @@ static_assert(PXB_MAX_STEP_CAP <= 8192, "14-bit packed tickets / steps");
 #ifndef PXB_OCC_P1
 #define PXB_OCC_P1 4
 #endif
+#ifndef PXB_OCC_P1_FF
+#define PXB_OCC_P1_FF 6   // measured on config 2: 4 -> 6 is +6 % (80 VGPRs, 12-wave blocks); 5 is 30 % slower
+#endif
 #ifndef PXB_OCC_P2
 #define PXB_OCC_P2 4   // measured: 3 -> 4 is +10 % on configs 3, 4; 5, 6 no better
 #endif
 #ifndef PXB_OCC_P3
-#define PXB_OCC_P3 2
+#define PXB_OCC_P3 3   // measured: 2 -> 3 is +25 % on config 5 (VGPRs fit 3 waves without spills)
 #endif
 // Faulty kernels hand out instances from a device work queue in chunks of
 // QCHUNK (instance lengths vary from a few steps to step_cap, so a static
@@ -200,10 +203,11 @@ __device__ __forceinline__ uint32_t code32(uint32_t v) {
   else return v ? ((v << 24) | 1u) : 0u;
 }
 
-// occupancy target (waves per SIMD) by proposer count: bounds the VGPR budget
-template <int PM> struct Occ { static constexpr int waves = PXB_OCC_P1; };
-template <> struct Occ<2> { static constexpr int waves = PXB_OCC_P2; };
-template <> struct Occ<3> { static constexpr int waves = PXB_OCC_P3; };
+// occupancy target (waves per SIMD) by proposer count and schedule kind:
+// bounds the VGPR budget (launch bounds) and the host's residency
+template <int PM, bool FF> struct Occ {
+  static constexpr int waves = PM == 1 ? (FF ? PXB_OCC_P1_FF : PXB_OCC_P1) : PM == 2 ? PXB_OCC_P2 : PXB_OCC_P3;
+};
 
 // Waves per block (LDS is carved per wave).  Faulty kernels: one wave per
 // block, balanced by the device work queue.  Fault-free kernels: as many of a
@@ -216,18 +220,20 @@ constexpr int LDS_BYTES = 163840;
 template <int PM, int N, bool LOGM, bool FF>
 struct Shape {
   static constexpr int lds = (int)sizeof(Lds<PM, N, LOGM>);
-  static constexpr int cap = 4 * Occ<PM>::waves;   // waves per CU at the occupancy target
+  static constexpr int occ = Occ<PM, FF>::waves;
+  static constexpr int cap = 4 * occ;              // waves per CU at the occupancy target
 #ifdef PXB_WPB
   static constexpr int wpb = PXB_WPB;
 #else
-  // waves resident per CU with w waves per block (LDS- and target-limited)
+  // waves resident per CU with w waves per block: whole blocks, LDS- and
+  // target-limited
   static constexpr int resident(int w) {
-    return (w * lds > LDS_BYTES || w > cap) ? 0 : ((LDS_BYTES / (w * lds)) * w < cap ? (LDS_BYTES / (w * lds)) * w : cap);
+    return (w * lds > LDS_BYTES) ? 0 : ((LDS_BYTES / (w * lds)) < (cap / w) ? (LDS_BYTES / (w * lds)) : (cap / w)) * w;
   }
-  // the largest power-of-two block that keeps the most waves resident
+  // the largest block (<= 16 waves) that keeps the most waves resident
   static constexpr int best() {
     int b = 1;
-    for (int w = 2; w <= 16; w *= 2)
+    for (int w = 2; w <= 16; ++w)
       if (resident(w) >= resident(b)) b = w;
     return b;
   }
@@ -258,7 +264,7 @@ __device__ __forceinline__ uint4 philox_here(uint32_t c0, uint32_t c1, uint32_t 
 // count is its length (requests) or its length before this step's acceptor
 // phase (responses), and no Philox draw, due-nibble or isolation test is needed.
 template <int PM, int N, bool LOGM, bool FF>
-__global__ __launch_bounds__((Shape<PM, N, LOGM, FF>::block), Occ<PM>::waves) void paxos_batch_kernel(KParams kp) {
+__global__ __launch_bounds__((Shape<PM, N, LOGM, FF>::block), (Occ<PM, FF>::waves)) void paxos_batch_kernel(KParams kp) {
   constexpr int WPB = Shape<PM, N, LOGM, FF>::wpb;
   constexpr int G = 64 / N;
   constexpr uint32_t NM = (1u << N) - 1u;     // slot-local lane mask

@@ -2,9 +2,9 @@
 (tools/profile_round.sh, valu/) and the kernel-trace average duration.
 
 The batch kernel keeps the protocol state on chip, so its real limiter is
-VALU issue, not HBM.  A wave64 VALU instruction occupies its SIMD's 16 lanes
-for 4 cycles, so a CU issues at most one wave-instruction per cycle over its 4
-SIMDs: peak = CUs x clock.  The clock is the in-kernel effective clock,
+VALU issue, not HBM.  Nominally a wave64 VALU instruction occupies its SIMD's
+16 lanes for 4 cycles (one wave-instruction per CU-cycle); the measured
+ceiling for simple 32-bit ops is higher (profiles/r01_valu_peak.jsonl).  The clock is the in-kernel effective clock,
 GRBM_GUI_ACTIVE / 8 XCDs / kernel time (MI355X_MICROARCH.md, DVFS give-back),
 capped at 2.4 GHz.
     python tools/valu_roofline.py <prof dir> <instances per launch> [out.json]"""
@@ -37,14 +37,25 @@ def roofline(root, instances):
     clock_hz = min(s["GRBM_GUI_ACTIVE"] / 8.0 / (ns * 1e-9), 2.4e9)
     rate = s["SQ_INSTS_VALU"] / (ns * 1e-9)               # wave-instructions / s
     peak = CUS * clock_hz
+    # measured ceiling: tools/micro/valu_peak.hip (independent add/xor chains,
+    # 8 waves/SIMD) issues ~1.4 wave-instructions per CU-cycle on gfx950
+    emp = None
+    pf = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "r01_valu_peak.jsonl")
+    if os.path.exists(pf):
+        rows = [json.loads(line) for line in open(pf) if line.strip()]
+        emp = max(r["G_wave_valu_insts_per_s"] for r in rows if r["kernel"] == "add/xor chains") * 1e9
     return {"kernel_avg_us": ns / 1e3, "effective_clock_MHz": clock_hz / 1e6,
             "valu_insts_per_launch": s["SQ_INSTS_VALU"], "valu_insts_per_instance": s["SQ_INSTS_VALU"] / instances,
             "lds_insts_per_instance": s["SQ_INSTS_LDS"] / instances,
             "salu_insts_per_instance": s["SQ_INSTS_SALU"] / instances,
             "achieved_G_wave_insts_per_s": rate / 1e9, "peak_G_wave_insts_per_s": peak / 1e9,
-            "valu_issue_frac": rate / peak,
-            "note": "peak = 256 CUs x effective clock x 1 wave64 VALU instruction per CU-cycle (4 SIMDs x 16 lanes, "
-                    "4 cycles per wave64 instruction); PMC means per dispatch"}
+            "frac_of_1_per_CU_cycle": rate / peak,
+            "measured_ceiling_G_wave_insts_per_s": None if emp is None else emp / 1e9,
+            "valu_issue_frac": None if emp is None else rate / emp,
+            "note": "1 wave64 VALU instruction per CU-cycle (4 SIMDs x 16 lanes, 4 cycles each) is the nominal "
+                    "rate; gfx950 issues simple 32-bit ops faster (tools/micro/valu_peak.hip: 1.4 per CU-cycle "
+                    "for add/xor chains, 0.98 for select chains), so valu_issue_frac is against that measured "
+                    "add/xor ceiling; PMC means per dispatch"}
 
 
 if __name__ == "__main__":
