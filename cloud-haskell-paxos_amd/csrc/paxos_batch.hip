@@ -302,8 +302,11 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
   // lengths), 60000 for the work-queue kernels (which also flush mid-run);
   // epoch tags (idx + 1 under the work queue) stay below 2^30
   const uint64_t wpb = (uint64_t)fn.wpb;
-  const uint64_t chunk_max = ff ? std::min<uint64_t>(1ull << 31, resident * wpb * G * 30000ull)
-                                : std::min<uint64_t>((1ull << 30) - 1, resident * wpb * G * 60000ull);
+  // fault-free log mode: 16-bit epochs, so every block's range (static slices:
+  // every wave's) stays below 2^16 instances
+  const uint64_t chunk_max = (ff && logm) ? std::min<uint64_t>(resident * wpb * G * 30000ull, resident * 60000ull)
+                             : ff ? std::min<uint64_t>(1ull << 31, resident * wpb * G * 30000ull)
+                                  : std::min<uint64_t>((1ull << 30) - 1, resident * wpb * G * 60000ull);
   for (uint64_t done = 0; done < cfg->n_instances; done += chunk_max) {
     const uint64_t nc = std::min<uint64_t>(chunk_max, cfg->n_instances - done);
     kp.first_instance = cfg->first_instance + done;

@@ -185,10 +185,19 @@ __device__ __forceinline__ void l_pop_n(Link& L, uint32_t n) {
 template <int PM, bool LOGM> struct Ring2 { uint32_t w[PM][QD][64]; };
 template <int PM> struct Ring2<PM, false> { uint32_t w[1][1][1]; };
 
-template <int PM, int N, bool LOGM>
+// Canonical-log entry (epoch << CB | command).  Single decree: 2-bit clientId,
+// 30-bit epochs.  Log mode: 16-bit commands; the fault-free kernels keep each
+// wave's / block's instance range below 2^16 (host) so the entry fits 32 bits
+// (half the LDS: config 6 goes from 7 to 9 resident waves per CU); the queue
+// kernels' epochs need 32 bits and a 64-bit entry.
+template <bool LOGM, bool FF> struct ClogFmt { using type = uint32_t; static constexpr uint32_t cb = 2u; };
+template <> struct ClogFmt<true, true> { using type = uint32_t; static constexpr uint32_t cb = 16u; };
+template <> struct ClogFmt<true, false> { using type = unsigned long long; static constexpr uint32_t cb = 32u; };
+
+template <int PM, int N, bool LOGM, bool FF>
 struct Lds {
   static constexpr int G = 64 / N;
-  using clog_t = std::conditional_t<LOGM, unsigned long long, uint32_t>;
+  using clog_t = typename ClogFmt<LOGM, FF>::type;
   uint32_t rq[PM][QD][64];       // links p -> a   (lane-interleaved: conflict-free)
   uint32_t sq[PM][QD][64];       // links a -> p
   clog_t clog[G][LT + 1];        // per-slot canonical log (+1 pad: rows on distinct banks);
@@ -219,7 +228,7 @@ template <int PM, bool FF> struct Occ {
 constexpr int LDS_BYTES = 163840;
 template <int PM, int N, bool LOGM, bool FF>
 struct Shape {
-  static constexpr int lds = (int)sizeof(Lds<PM, N, LOGM>);
+  static constexpr int lds = (int)sizeof(Lds<PM, N, LOGM, FF>);
   static constexpr int occ = Occ<PM, FF>::waves;
   static constexpr int cap = 4 * occ;              // waves per CU at the occupancy target
 #ifdef PXB_WPB
@@ -272,17 +281,17 @@ __global__ __launch_bounds__((Shape<PM, N, LOGM, FF>::block), (Occ<PM, FF>::wave
   // command field of a request word: single decree = clientId (2 bits, t = 1),
   // log mode = id << 14 | t (16 bits); the kind sits above it
   constexpr uint32_t ZM = LOGM ? 0xFFFFu : 3u, KSH = LOGM ? 30u : 16u;
-  using clog_t = typename Lds<PM, N, LOGM>::clog_t;
-  constexpr uint32_t CB = LOGM ? 32u : 2u;    // epoch shift of a canonical-log entry
+  using clog_t = typename Lds<PM, N, LOGM, FF>::clog_t;
+  constexpr uint32_t CB = ClogFmt<LOGM, FF>::cb;   // epoch shift of a canonical-log entry
   // A lone proposer on a fault-free schedule is never NACKed (its tickets only
   // grow and nobody else raises T_max) and gets at most one response per link
   // per step, so the NACK handling and the multi-response fold compile out.
   constexpr bool CONTENDED = !(FF && PM == 1);
-  __shared__ Lds<PM, N, LOGM> s_lds[WPB];
+  __shared__ Lds<PM, N, LOGM, FF> s_lds[WPB];
 
   const int lane = threadIdx.x & 63;
   const int wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  Lds<PM, N, LOGM>& L = s_lds[wib];
+  Lds<PM, N, LOGM, FF>& L = s_lds[wib];
   const int g = lane / N;
   const int a = lane - g * N;
   const bool used = g < G;

@@ -110,6 +110,16 @@ def test_ragged_batch_sizes(gpu_lib, n):
     _cmp(pxb.CONFIGS[3], 5, n)
 
 
+@pytest.mark.parametrize("n", [1, 11, 12, 13, 143, 144, 145, 4097, 50001])
+@pytest.mark.parametrize("c", [2, 6, "p3"])
+def test_ragged_block_queue_sizes(gpu_lib, c, n):
+    """Fault-free kernels run multi-wave blocks that share the block's range
+    through an LDS counter, one slot-generation (G instances) per grab: batch
+    sizes around G, the block width and the grid edge."""
+    cfg = pxb.Config(seed=0x3F, n_proposers=3, n_acceptors=4, skew_max=2) if c == "p3" else pxb.CONFIGS[c]
+    _cmp(cfg, 9, n)
+
+
 def test_instance_ids_cross_32bit(gpu_lib):
     _cmp(pxb.CONFIGS[3], (1 << 32) - 3000, 6000)
 
