@@ -93,11 +93,12 @@ def test_log_mode_matches_oracle(gpu_lib, P, N, loss, delay, ticks, period, cras
     assert cnt["executes"] >= cnt["decided"]
 
 
-def test_log_mode_full_size_properties(gpu_lib):
-    """Fault-free log mode at 2^20 instances: every one of the 8 Ticks commits
-    its own command, so every acceptor log is c1.1 .. c1.8."""
+@pytest.mark.parametrize("n", [1 << 20, 1 << 25])
+def test_log_mode_full_size_properties(gpu_lib, n):
+    """Fault-free log mode: every one of the 8 Ticks commits its own command,
+    so every acceptor log is c1.1 .. c1.8.  2^25 instances take two launches
+    (16-bit canonical-log epochs cap a launch at 60000 instances per block)."""
     cfg = pxb.Config(seed=0x5EED0006, n_proposers=1, n_acceptors=5, n_ticks=8, tick_period=6)
-    n = 1 << 20
     res, dig, _, cnt = pxb.run(cfg, 0, n)
     assert cnt["executes"] == 8 * n and cnt["rounds"] == 8 * n and cnt["decided"] == n
     assert (res[:, 3] == ((7 * 6 + 6) << 16)).all()
