@@ -65,7 +65,8 @@ static_assert(PXB_MAX_STEP_CAP <= 8192, "14-bit packed tickets / steps");
 // fault-free kernels keep their static slices (a queue there costs 4x: every
 // wave would hit the counter every ~12 steps).
 #ifndef PXB_QCHUNK
-#define PXB_QCHUNK 16   // measured: 8 = 16 > 32 > 64 > 256 on configs 3-5
+#define PXB_QCHUNK 8    // measured: 8 = 16 > 32 > 64 > 256 on configs 3-5; under the
+                        // iterative-ILP scheduler 8 is +2 % on config 5, +0.5 % on 3/4
 #endif
 constexpr uint32_t QCHUNK = PXB_QCHUNK;
 // Run totals: each wave adds its counts into row (wave % TCOPIES) of a
