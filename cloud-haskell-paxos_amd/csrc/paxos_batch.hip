@@ -14,6 +14,7 @@
 #include <string.h>
 
 #include "../../include/paxos_batch.h"
+#include "paxos_ev_kernel.h"
 #include "paxos_kernel.h"
 
 namespace pxb {
@@ -28,6 +29,12 @@ namespace pxb {
 PXB_FOR_MODES(PXB_EXTERN, 1)
 PXB_FOR_MODES(PXB_EXTERN, 2)
 PXB_FOR_MODES(PXB_EXTERN, 3)
+// per-lane kernels (paxos_ev.hip): P x N x {8, 16}-step wheels
+#define PXB_EV_EXTERN(PM, N, W) extern template __global__ void ev::paxos_ev_kernel<PM, N, W>(ev::EvKParams);
+#define PXB_EV_FOR(M, PM, W) M(PM, 2, W) M(PM, 3, W) M(PM, 4, W) M(PM, 5, W) M(PM, 6, W) M(PM, 7, W) M(PM, 8, W) M(PM, 9, W)
+PXB_EV_FOR(PXB_EV_EXTERN, 1, 8) PXB_EV_FOR(PXB_EV_EXTERN, 1, 16)
+PXB_EV_FOR(PXB_EV_EXTERN, 2, 8) PXB_EV_FOR(PXB_EV_EXTERN, 2, 16)
+PXB_EV_FOR(PXB_EV_EXTERN, 3, 8) PXB_EV_FOR(PXB_EV_EXTERN, 3, 16)
 
 // ---- single-handler hook kernels ------------------------------------------
 __global__ void acceptor_hook_kernel(pxb_acceptor_rec* st, const pxb_msg* in, pxb_msg* out, uint32_t count) {
@@ -66,11 +73,15 @@ __global__ void proposer_hook_kernel(pxb_proposer_rec* st, uint32_t n_acc, const
   nb[i] = no;
 }
 
+constexpr uint32_t QWORDS = 4;          // per-slot queue / counter words (finalize_kernel resets them)
+
 // Sums the TCOPIES partial rows into the caller's totals, zeroes them and
 // resets the work queue, so the launch slot is clean for its next use.  One
 // block of TCOPIES threads; thread t reads column t % 16 of rows t/16, t/16+16, ...
 __global__ __launch_bounds__(TCOPIES) void finalize_kernel(unsigned long long* part, uint32_t* queue,
                                                             unsigned long long* totals) {
+  // queue words: [0] general kernel's work queue, [1] per-lane kernel's work
+  // queue, [2] its bailed-instance count
   __shared__ unsigned long long acc[16];
   const uint32_t t = threadIdx.x;
   if (t < 16) acc[t] = 0ull;
@@ -84,11 +95,39 @@ __global__ __launch_bounds__(TCOPIES) void finalize_kernel(unsigned long long* p
   if (v) atomicAdd(&acc[t % 16u], v);
   __syncthreads();
   if (t < 16 && acc[t]) atomicAdd(&totals[t], acc[t]);
-  if (t == 16 && queue) queue[0] = 0u;
+  if (t >= 16 && t < 16 + QWORDS && queue) queue[t - 16] = 0u;
 }
 
 // ---- host side ----------------------------------------------------------------
 typedef void (*kernel_ptr)(KParams);
+typedef void (*ev_kernel_ptr)(ev::EvKParams);
+
+template <int PM, int W>
+static ev_kernel_ptr ev_pick_n(uint32_t n) {
+  switch (n) {
+    case 2: return ev::paxos_ev_kernel<PM, 2, W>;
+    case 3: return ev::paxos_ev_kernel<PM, 3, W>;
+    case 4: return ev::paxos_ev_kernel<PM, 4, W>;
+    case 5: return ev::paxos_ev_kernel<PM, 5, W>;
+    case 6: return ev::paxos_ev_kernel<PM, 6, W>;
+    case 7: return ev::paxos_ev_kernel<PM, 7, W>;
+    case 8: return ev::paxos_ev_kernel<PM, 8, W>;
+    case 9: return ev::paxos_ev_kernel<PM, 9, W>;
+  }
+  return nullptr;
+}
+
+static ev_kernel_ptr ev_pick(uint32_t pm, uint32_t n, int w) {
+  switch (pm * 100 + (uint32_t)w) {
+    case 108: return ev_pick_n<1, 8>(n);
+    case 116: return ev_pick_n<1, 16>(n);
+    case 208: return ev_pick_n<2, 8>(n);
+    case 216: return ev_pick_n<2, 16>(n);
+    case 308: return ev_pick_n<3, 8>(n);
+    case 316: return ev_pick_n<3, 16>(n);
+  }
+  return nullptr;
+}
 struct kernel_fn {
   kernel_ptr fn;
   int wpb;                       // waves per block (Shape<>::wpb)
@@ -146,6 +185,11 @@ constexpr int QSLOTS = 64;
 constexpr size_t SLOT_U64 = (size_t)TCOPIES * 16 + 16;
 static unsigned long long* g_slots[64];
 static uint32_t g_qseq[64];
+// per-lane kernel: bailed-id buffer of each scratch slot (lazily allocated),
+// blocks per CU by [wheel][pm][n][device]
+constexpr uint64_t EV_CHUNK = 1ull << 21;
+static uint32_t* g_bail[64][QSLOTS];
+static int g_eocc[2][4][10][64];
 
 static int hip_fail(hipError_t e) {
   g_last_hip = (int)e;
@@ -232,10 +276,17 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
   // to an isolated acceptor (Tick skew is allowed)
   const bool ff = !(cfg->flags & PXB_CFG_RANDOMIZE) && cfg->loss_ppm == 0 && cfg->delay_max == 1 &&
                   cfg->crash_ppm == 0;
+  // faulty single-decree batches run on the per-lane kernel (paxos_ev.h), its
+  // bailed instances on the general faulty kernel; PXB_NO_EV=1 forces the latter
+  const char* no_ev = getenv("PXB_NO_EV");
+  const bool use_ev = !ff && !logm && ev::eligible(cfg) && !(no_ev && atoi(no_ev) > 0);
   kernel_fn fn = pick(cfg->n_proposers, cfg->n_acceptors, logm, ff);
   if (!fn) return PXB_E_INVAL;
+  const int wheel = ev::wheel_for(cfg->delay_max);
+  const ev_kernel_ptr efn = use_ev ? ev_pick(cfg->n_proposers, cfg->n_acceptors, wheel) : nullptr;
+  if (use_ev && !efn) return PXB_E_INVAL;
   const hipStream_t st = (hipStream_t)stream;
-  int occ, cus;
+  int occ, cus, eocc = 0;
   {
     std::lock_guard<std::mutex> lk(g_mu);
     if (!g_cus[dev]) {
@@ -255,6 +306,15 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
     const int target = 4 * fn.occ;
     occ = std::min(o, std::max(1, target / fn.wpb));   // blocks per CU
     cus = g_cus[dev];
+    if (use_ev) {
+      int& eo = g_eocc[(wheel == 8) ? 0 : 1][cfg->n_proposers][cfg->n_acceptors][dev];
+      if (!eo) {
+        int nb = 0;
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)efn, 64, 0));
+        eo = std::max(1, nb);
+      }
+      eocc = eo;
+    }
     if (!g_slots[dev]) {
       unsigned long long* q = nullptr;
       HIPCHK(hipMalloc(&q, QSLOTS * SLOT_U64 * sizeof(unsigned long long)));
@@ -263,7 +323,10 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
       g_slots[dev] = q;
     }
     const char* cap_env = getenv("PXB_BLOCKS_PER_CU");   // tests / experiments: cap residency
-    if (cap_env && atoi(cap_env) > 0) occ = std::min(occ, atoi(cap_env));
+    if (cap_env && atoi(cap_env) > 0) {
+      occ = std::min(occ, atoi(cap_env));
+      if (eocc) eocc = std::min(eocc, atoi(cap_env));
+    }
   }
   KParams kp;
   memset(&kp, 0, sizeof(kp));
@@ -300,11 +363,13 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
   // a launch must not give any slot 65536 instances (16-bit packed run totals):
   // on average 30000 per slot for the block-queue kernels (uniform instance
   // lengths), 60000 for the work-queue kernels (which also flush mid-run);
-  // epoch tags (idx + 1 under the work queue) stay below 2^30
+  // epoch tags (idx + 1 under the work queue) stay below 2^30.  Per-lane
+  // chunks are bounded by the bailed-id buffer of a scratch slot.
   const uint64_t wpb = (uint64_t)fn.wpb;
   // fault-free log mode: 16-bit epochs, so every block's range (static slices:
   // every wave's) stays below 2^16 instances
-  const uint64_t chunk_max = (ff && logm) ? std::min<uint64_t>(resident * wpb * G * 30000ull, resident * 60000ull)
+  const uint64_t chunk_max = use_ev ? (uint64_t)EV_CHUNK
+                             : (ff && logm) ? std::min<uint64_t>(resident * wpb * G * 30000ull, resident * 60000ull)
                              : ff ? std::min<uint64_t>(1ull << 31, resident * wpb * G * 30000ull)
                                   : std::min<uint64_t>((1ull << 30) - 1, resident * wpb * G * 60000ull);
   for (uint64_t done = 0; done < cfg->n_instances; done += chunk_max) {
@@ -314,24 +379,55 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
     kp.out = d_out ? reinterpret_cast<uint4*>(d_out + done) : nullptr;
     kp.dig = d_log_digest ? d_log_digest + done * cfg->n_acceptors : nullptr;
     kp.acc = d_acc ? reinterpret_cast<uint4*>(d_acc + done * cfg->n_acceptors) : nullptr;
+    uint32_t* bail = nullptr;
+    int sidx;
     {
       std::lock_guard<std::mutex> lk(g_mu);
-      unsigned long long* slot = g_slots[dev] + (size_t)(g_qseq[dev]++ % QSLOTS) * SLOT_U64;
+      sidx = (int)(g_qseq[dev]++ % QSLOTS);
+      unsigned long long* slot = g_slots[dev] + (size_t)sidx * SLOT_U64;
       kp.part = slot;
       kp.queue = reinterpret_cast<uint32_t*>(slot + (size_t)TCOPIES * 16);
+      if (use_ev) {
+        if (!g_bail[dev][sidx]) HIPCHK(hipMalloc(&g_bail[dev][sidx], (size_t)EV_CHUNK * sizeof(uint32_t)));
+        bail = g_bail[dev][sidx];
+      }
     }
-    const uint64_t waves_needed = (nc + G - 1) / G;
-    const uint64_t blocks_needed = (waves_needed + wpb - 1) / wpb;
-    const unsigned grid = (unsigned)std::min<uint64_t>(blocks_needed, resident);
+    if (use_ev) {
+      // the per-lane kernel over the chunk, then the general kernel over its bailed ids
+      ev::EvKParams ek;
+      memset(&ek, 0, sizeof(ek));
+      ek.p = ev::make_params(cfg);
+      ek.p.first_instance = kp.first_instance;
+      ek.n_instances = (uint32_t)nc;
+      ek.out = kp.out;
+      ek.dig = kp.dig;
+      ek.acc = kp.acc;
+      ek.part = kp.part;
+      ek.queue = kp.queue + 1;
+      ek.bail_ids = bail;
+      ek.bail_n = kp.queue + 2;
+      const uint64_t eres = (uint64_t)eocc * (uint64_t)cus;
+      const unsigned egrid = (unsigned)std::min<uint64_t>((nc + 63) / 64, eres);
+      hipLaunchKernelGGL(efn, dim3(egrid), dim3(64), 0, st, ek);
+      HIPCHK(hipGetLastError());
+      kp.ids = bail;
+      kp.n_ids = kp.queue + 2;
+      hipLaunchKernelGGL(fn.fn, dim3((unsigned)resident), dim3(64 * fn.wpb), 0, st, kp);
+      HIPCHK(hipGetLastError());
+    } else {
+      const uint64_t waves_needed = (nc + G - 1) / G;
+      const uint64_t blocks_needed = (waves_needed + wpb - 1) / wpb;
+      const unsigned grid = (unsigned)std::min<uint64_t>(blocks_needed, resident);
 #ifdef PXB_WAVE_TIMES
-    if (!g_wt) HIPCHK(hipMalloc(&g_wt, 6ull * 65536 * sizeof(unsigned long long)));
-    kp.dbg = g_wt;
-    g_wt_waves = grid * fn.wpb;
-    if (grid * fn.wpb > 65536) return PXB_E_INVAL;
+      if (!g_wt) HIPCHK(hipMalloc(&g_wt, 6ull * 65536 * sizeof(unsigned long long)));
+      kp.dbg = g_wt;
+      g_wt_waves = grid * fn.wpb;
+      if (grid * fn.wpb > 65536) return PXB_E_INVAL;
 #endif
-    hipLaunchKernelGGL(fn.fn, dim3(grid), dim3(64 * fn.wpb), 0, st, kp);
-    HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(TCOPIES), 0, st, kp.part, ff ? nullptr : kp.queue, totals);
+      hipLaunchKernelGGL(fn.fn, dim3(grid), dim3(64 * fn.wpb), 0, st, kp);
+      HIPCHK(hipGetLastError());
+    }
+    hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(TCOPIES), 0, st, kp.part, kp.queue, totals);
     HIPCHK(hipGetLastError());
   }
   return PXB_OK;

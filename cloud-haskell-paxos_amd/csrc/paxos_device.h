@@ -26,7 +26,7 @@ constexpr uint32_t IDLE = 0, ROUND1 = 1, ROUND2 = 2;
 // Each round needs the full 64-bit products of two 32-bit words: written as
 // 64-bit multiplies they compile to one v_mad_u64_u32 each instead of a
 // v_mul_lo_u32 + v_mul_hi_u32 pair.
-__device__ __forceinline__ uint4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+__host__ __device__ __forceinline__ uint4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                         uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
@@ -42,9 +42,11 @@ __device__ __forceinline__ uint4 philox(uint32_t c0, uint32_t c1, uint32_t c2, u
   return make_uint4(c0, c1, c2, c3);
 }
 
-__device__ __forceinline__ uint32_t mulhi_n(uint32_t w, uint32_t n) { return __umulhi(w, n); }
+__host__ __device__ __forceinline__ uint32_t mulhi_n(uint32_t w, uint32_t n) {
+  return (uint32_t)(((uint64_t)w * n) >> 32);   // v_mul_hi_u32 on the device
+}
 
-__device__ __forceinline__ uint32_t fnv_u32(uint32_t h, uint32_t v) {
+__host__ __device__ __forceinline__ uint32_t fnv_u32(uint32_t h, uint32_t v) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     h ^= (v >> (8 * i)) & 0xFFu;

@@ -1,0 +1,155 @@
+// paxos_ev_kernel.h — gfx950 wave driver of the per-lane kernel (paxos_ev.h).
+//
+// One 64-lane wave per block, persistent: every lane runs its own instance one
+// micro-step per iteration and, when the instance ends (or bails), writes its
+// outputs and takes the next instance id from the wave's chunk of the launch's
+// work queue.  The per-lane state lives in the block's LDS, lane-interleaved.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "paxos_ev.h"
+
+namespace pxb {
+namespace ev {
+
+// lane-interleaved LDS words: word i of lane l at w[i * 64 + l]
+struct LdsMem {
+  uint32_t* w;
+  uint32_t lane;
+  __host__ __device__ uint32_t ld(uint32_t i) const { return w[i * 64u + lane]; }
+  __host__ __device__ void st(uint32_t i, uint32_t v) const { w[i * 64u + lane] = v; }
+  // halfword i of the array starting at word `base`
+  __host__ __device__ uint32_t ld16(uint32_t base, uint32_t i) const {
+    return reinterpret_cast<const uint16_t*>(w)[((base + (i >> 1)) * 64u + lane) * 2u + (i & 1u)];
+  }
+  __host__ __device__ void st16(uint32_t base, uint32_t i, uint32_t v) const {
+    reinterpret_cast<uint16_t*>(w)[((base + (i >> 1)) * 64u + lane) * 2u + (i & 1u)] = (uint16_t)v;
+  }
+};
+
+constexpr uint32_t EV_QCHUNK = 64;            // instances per work-queue grab (one per lane)
+constexpr uint32_t EV_TCOPIES = 256;          // partial-total rows (= TCOPIES in paxos_kernel.h)
+
+struct EvKParams {
+  EvParams p;
+  uint32_t n_instances;
+  uint4* out;                                 // pxb_result records (nullable)
+  uint32_t* dig;                              // log digests (nullable)
+  uint4* acc;                                 // final acceptor records (nullable)
+  unsigned long long* part;                   // EV_TCOPIES partial run-total rows
+  uint32_t* queue;                            // next instance, 0 on entry
+  uint32_t* bail_ids;                         // ids of bailed instances (capacity n_instances)
+  uint32_t* bail_n;                           // their count, 0 on entry
+};
+
+// pool / wheel sizes of a (PM, N, delay) shape
+template <int PM, int N> struct EvPool { static constexpr int value = (PM * N <= 16) ? 32 : 64; };
+
+template <int PM, int N, int W>
+__global__ __launch_bounds__(64, 1) void paxos_ev_kernel(EvKParams kp) {
+  constexpr int POOL = EvPool<PM, N>::value;
+  using S = Shape<PM, N, POOL, W>;
+  __shared__ uint32_t lds[S::WORDS * 64];
+  const uint32_t lane = threadIdx.x;
+  EvLane<PM, N, POOL, W, LdsMem> L;
+  L.m = LdsMem{lds, lane};
+  L.mode = M_IDLE;
+  L.bailed = false;
+  const uint32_t n = kp.n_instances;
+  const uint64_t below = (1ull << lane) - 1ull;
+  uint32_t next = 0, end = 0;
+  bool drained = false;
+  // lane totals over the instances this lane ran
+  uint32_t t_inst = 0, t_undec = 0, t_stuck = 0, t_panic = 0, t_div = 0, t_cap = 0;
+  uint32_t t_rounds = 0, t_steps = 0, t_msgs = 0, t_execs = 0;
+  unsigned long long t_canon = 0;
+
+  for (;;) {
+    // ---- refill idle lanes from the wave's chunk of the queue ----
+    uint64_t freeb = __builtin_amdgcn_ballot_w64(L.mode == M_IDLE);
+    while (freeb != 0ull && !drained) {
+      if (next >= end) {
+        uint32_t c = 0;
+        if (lane == 0) c = atomicAdd(kp.queue, EV_QCHUNK);
+        c = (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
+        if (c >= n) {
+          drained = true;
+          break;
+        }
+        next = c;
+        end = min(c + EV_QCHUNK, n);
+      }
+      const uint32_t take = min((uint32_t)__popcll(freeb), end - next);
+      const uint32_t rank = (uint32_t)__popcll(freeb & below);
+      if (((freeb >> lane) & 1ull) && rank < take) L.init(kp.p, next + rank);
+      next += take;
+      freeb = __builtin_amdgcn_ballot_w64(L.mode == M_IDLE);
+    }
+    if (__builtin_amdgcn_ballot_w64(L.mode != M_IDLE) == 0ull) break;
+
+    // ---- one micro-step of every live lane ----
+    if (L.mode != M_IDLE) {
+      EvOut o;
+      const bool done = L.step(kp.p, o);
+      if (L.bailed) {                         // beyond this kernel's capacities: re-run by the general kernel
+        const uint32_t pos = atomicAdd(kp.bail_n, 1u);
+        kp.bail_ids[pos] = L.gid;
+        L.mode = M_IDLE;
+        L.bailed = false;
+      } else if (done) {
+        const uint32_t f = o.flags;
+        t_inst += 1u;
+        t_undec += (f & PXB_F_UNDECIDED) ? 1u : 0u;
+        t_stuck += (f & PXB_F_STUCK) ? 1u : 0u;
+        t_panic += (f & PXB_F_PANIC) ? 1u : 0u;
+        t_div += (f & PXB_F_LOG_DIVERGENCE) ? 1u : 0u;
+        t_cap += (f & PXB_F_STEP_CAP) ? 1u : 0u;
+        t_rounds += L.rounds;
+        t_steps += o.steps;
+        t_msgs += L.msgs;
+        t_execs += L.execs;
+        t_canon += L.canon;
+        if (kp.out) kp.out[L.gid] = make_uint4(o.res[0], o.res[1], o.res[2], o.res[3]);
+        if (kp.dig) {
+#pragma unroll
+          for (int a = 0; a < N; ++a) kp.dig[(uint64_t)L.gid * N + a] = L.digest_of(a);
+        }
+        if (kp.acc) {
+#pragma unroll
+          for (int a = 0; a < N; ++a) {
+            uint32_t r[4];
+            L.record_of(a, r);
+            kp.acc[(uint64_t)L.gid * N + a] = make_uint4(r[0], r[1], r[2], r[3]);
+          }
+        }
+      }
+    }
+  }
+
+  // ---- run totals: wave reduction, one atomic per counter into a partial row ----
+  uint32_t v[11] = {t_inst, t_undec, t_stuck, t_panic, t_div, t_cap, t_rounds, t_steps, t_msgs, t_execs,
+                    t_inst - t_undec};
+  unsigned long long c64 = t_canon;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+#pragma unroll
+    for (int q = 0; q < 11; ++q) v[q] += (uint32_t)__shfl_xor((int)v[q], off);
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)c64, off);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(c64 >> 32), off);
+    c64 += ((unsigned long long)hi << 32) | lo;
+  }
+  unsigned long long* const trow = kp.part + (size_t)(blockIdx.x % EV_TCOPIES) * 16u;
+  if (lane < 11) {
+    const int slot_of[11] = {PXB_C_INSTANCES, PXB_C_UNDECIDED, PXB_C_STUCK, PXB_C_PANIC, PXB_C_DIVERGENCE,
+                             PXB_C_STEP_CAP, PXB_C_ROUNDS, PXB_C_STEPS, PXB_C_MESSAGES, PXB_C_EXECUTES,
+                             PXB_C_DECIDED};
+    unsigned long long val = 0;
+#pragma unroll
+    for (int q = 0; q < 11; ++q) val = (lane == (uint32_t)q) ? (unsigned long long)v[q] : val;
+    if (val) atomicAdd(&trow[slot_of[lane]], val);
+  }
+  if (lane == 11 && c64) atomicAdd(&trow[PXB_C_CANON_BYTES], c64);
+}
+
+}  // namespace ev
+}  // namespace pxb

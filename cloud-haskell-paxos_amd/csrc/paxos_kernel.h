@@ -100,6 +100,10 @@ struct KParams {
   unsigned long long* part;           // TCOPIES partial run-total rows (16 counters, 128 B each)
   uint32_t* queue;                    // faulty kernels: next instance, 0 on entry
   unsigned long long* dbg;            // diagnostic builds only (PXB_STAMPS)
+  // faulty kernels only: run the instances listed in ids[0 .. *n_ids) (the
+  // per-lane kernel's bailed instances, paxos_ev.h) instead of 0 .. n_instances
+  const uint32_t* ids;
+  const uint32_t* n_ids;
 };
 
 __host__ __device__ inline uint64_t prob_threshold(uint32_t ppm) {
@@ -305,7 +309,9 @@ __global__ __launch_bounds__((Shape<PM, N, LOGM, FF>::block), (Occ<PM, FF>::wave
 
   const uint32_t wave = blockIdx.x * WPB + wib;
   const uint32_t nwaves = gridDim.x * WPB;
-  const uint32_t n = kp.n_instances;
+  // faulty kernels may take their instances from a device-side list (its
+  // length is written by the kernel launched before this one)
+  const uint32_t n = (!FF && kp.n_ids) ? (uint32_t)__builtin_amdgcn_readfirstlane((int)*kp.n_ids) : kp.n_instances;
   // faulty kernels: chunks from the device work queue (DYN); fault-free
   // kernels: one-generation chunks of the block's contiguous range from an
   // LDS counter (BQ); diagnostic builds: a static slice per wave
@@ -341,7 +347,8 @@ __global__ __launch_bounds__((Shape<PM, N, LOGM, FF>::block), (Occ<PM, FF>::wave
   bool faulty = false, lossy = false, tovf = false;
   int32_t last_tick = 0;
   int32_t s = 0;                          // current step
-  uint32_t idx = 0;                       // local instance index
+  uint32_t idx = 0;                       // local instance index (queue position)
+  uint32_t gid = 0;                       // instance index within the launch (ids[idx] with a list)
   uint32_t loss_m1 = 0;
   uint32_t rounds = 0, dval = 0;          // dval: decided clientId (0 = none)
   int32_t dtick = 0;
@@ -439,7 +446,7 @@ __global__ __launch_bounds__((Shape<PM, N, LOGM, FF>::block), (Occ<PM, FF>::wave
     if (!FF && any(pred && faulty)) SCOUNT(5);
 #endif
     if (!FF && pred && faulty) {
-      const uint64_t inst = kp.first_instance + idx;
+      const uint64_t inst = kp.first_instance + gid;
       const uint4 w = philox_here((uint32_t)inst, (uint32_t)(inst >> 32), k, (1u << 24) | dirbits | (uint32_t)a, k0, k1);
       ok = !(lossy && w.x <= loss_m1);
       d = 1 + (int32_t)mulhi_n(w.y, dmax);
@@ -548,7 +555,8 @@ __global__ __launch_bounds__((Shape<PM, N, LOGM, FF>::block), (Occ<PM, FF>::wave
       const uint32_t cand = next + (uint32_t)__popcll(freeb & ((1ull << base) - 1ull));
       if (used && !active && cand < end) {
         idx = cand;
-        const uint64_t inst = kp.first_instance + cand;
+        gid = (!FF && kp.ids) ? kp.ids[cand] : cand;
+        const uint64_t inst = kp.first_instance + gid;
         const uint32_t ilo = (uint32_t)inst, ihi = (uint32_t)(inst >> 32);
         P = kp.n_prop;
         dmax = kp.delay_max;
@@ -1026,16 +1034,16 @@ __global__ __launch_bounds__((Shape<PM, N, LOGM, FF>::block), (Occ<PM, FF>::wave
           r.y = dval ? (uint32_t)dtick : 0u;
           r.z = rounds;
           r.w = (f & 0xFFu) | ((uint32_t)s << 16);
-          kp.out[idx] = r;
+          kp.out[gid] = r;
         }
-        if (kp.dig) kp.dig[(uint64_t)idx * N + a] = fnv_u32(digest, log_len);
+        if (kp.dig) kp.dig[(uint64_t)gid * N + a] = fnv_u32(digest, log_len);
         if (kp.acc) {
           uint4 r;
           r.x = (uint32_t)A.t_max;
           r.y = (uint32_t)A.t_store;
           r.z = code32<LOGM>(A.val);
           r.w = log_len | ((A.dead ? 1u : 0u) << 31);
-          kp.acc[(uint64_t)idx * N + a] = r;
+          kp.acc[(uint64_t)gid * N + a] = r;
         }
         active = false;
       }

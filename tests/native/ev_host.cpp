@@ -1,0 +1,115 @@
+// ev_host.cpp — TEST ONLY: runs the per-lane kernel's state machine
+// (cloud-haskell-paxos_amd/csrc/paxos_ev.h) on the host, one instance at a
+// time, so tests/test_ev_host.py can diff it against the CPU oracle without a
+// GPU.  The product runs the same EvLane code on the device
+// (paxos_ev_kernel.h); nothing here is linked into libpaxos_batch.so.
+#include <stdint.h>
+#include <string.h>
+
+#include <vector>
+
+#include "../../cloud-haskell-paxos_amd/csrc/paxos_ev.h"
+
+using namespace pxb;
+using namespace pxb::ev;
+
+namespace {
+
+struct HostMem {
+  uint32_t* w;
+  uint32_t ld(uint32_t i) const { return w[i]; }
+  void st(uint32_t i, uint32_t v) const { w[i] = v; }
+  uint32_t ld16(uint32_t base, uint32_t i) const { return reinterpret_cast<const uint16_t*>(w + base)[i]; }
+  void st16(uint32_t base, uint32_t i, uint32_t v) const { reinterpret_cast<uint16_t*>(w + base)[i] = (uint16_t)v; }
+};
+
+template <int PM, int N, int W>
+int run_shape(const pxb_config* cfg, pxb_result* out, uint32_t* dig, pxb_acceptor_rec* acc, int64_t* tot,
+              uint32_t* bail_ids, uint32_t* n_bail, uint64_t* micro_steps) {
+  constexpr int POOL = (PM * N <= 16) ? 32 : 64;
+  using S = Shape<PM, N, POOL, W>;
+  std::vector<uint32_t> buf(S::WORDS + 1, 0xDEADBEEFu);   // garbage: init must set what it reads
+  const EvParams p = make_params(cfg);
+  EvLane<PM, N, POOL, W, HostMem> L;
+  L.m = HostMem{buf.data()};
+  uint32_t nb = 0;
+  uint64_t ms = 0;
+  for (uint32_t g = 0; g < (uint32_t)cfg->n_instances; ++g) {
+    L.init(p, g);
+    EvOut o;
+    uint64_t guard = 0;
+    for (;;) {
+      const bool done = L.step(p, o);
+      ++ms;
+      if (++guard > 100000ull * cfg->step_cap) return -100;   // a hang is a test failure
+      if (L.bailed) {
+        bail_ids[nb++] = g;
+        break;
+      }
+      if (done) {
+        if (out) memcpy(&out[g], o.res, 16);
+        for (int a = 0; a < N; ++a) {
+          if (dig) dig[(uint64_t)g * N + a] = L.digest_of(a);
+          if (acc) {
+            uint32_t r[4];
+            L.record_of(a, r);
+            memcpy(&acc[(uint64_t)g * N + a], r, 16);
+          }
+        }
+        const uint32_t f = o.flags;
+        tot[PXB_C_INSTANCES] += 1;
+        tot[PXB_C_DECIDED] += !(f & PXB_F_UNDECIDED);
+        tot[PXB_C_UNDECIDED] += !!(f & PXB_F_UNDECIDED);
+        tot[PXB_C_STUCK] += !!(f & PXB_F_STUCK);
+        tot[PXB_C_PANIC] += !!(f & PXB_F_PANIC);
+        tot[PXB_C_DIVERGENCE] += !!(f & PXB_F_LOG_DIVERGENCE);
+        tot[PXB_C_STEP_CAP] += !!(f & PXB_F_STEP_CAP);
+        tot[PXB_C_ROUNDS] += L.rounds;
+        tot[PXB_C_STEPS] += o.steps;
+        tot[PXB_C_MESSAGES] += L.msgs;
+        tot[PXB_C_EXECUTES] += L.execs;
+        tot[PXB_C_CANON_BYTES] += L.canon;
+        break;
+      }
+    }
+  }
+  *n_bail = nb;
+  if (micro_steps) *micro_steps = ms;
+  return 0;
+}
+
+template <int PM, int W>
+int run_n(const pxb_config* c, pxb_result* o, uint32_t* d, pxb_acceptor_rec* a, int64_t* t, uint32_t* b, uint32_t* nb,
+          uint64_t* ms) {
+  switch (c->n_acceptors) {
+    case 2: return run_shape<PM, 2, W>(c, o, d, a, t, b, nb, ms);
+    case 3: return run_shape<PM, 3, W>(c, o, d, a, t, b, nb, ms);
+    case 4: return run_shape<PM, 4, W>(c, o, d, a, t, b, nb, ms);
+    case 5: return run_shape<PM, 5, W>(c, o, d, a, t, b, nb, ms);
+    case 6: return run_shape<PM, 6, W>(c, o, d, a, t, b, nb, ms);
+    case 7: return run_shape<PM, 7, W>(c, o, d, a, t, b, nb, ms);
+    case 8: return run_shape<PM, 8, W>(c, o, d, a, t, b, nb, ms);
+    case 9: return run_shape<PM, 9, W>(c, o, d, a, t, b, nb, ms);
+  }
+  return -1;
+}
+
+template <int W>
+int run_w(const pxb_config* c, pxb_result* o, uint32_t* d, pxb_acceptor_rec* a, int64_t* t, uint32_t* b, uint32_t* nb,
+          uint64_t* ms) {
+  switch (c->n_proposers) {
+    case 1: return run_n<1, W>(c, o, d, a, t, b, nb, ms);
+    case 2: return run_n<2, W>(c, o, d, a, t, b, nb, ms);
+    case 3: return run_n<3, W>(c, o, d, a, t, b, nb, ms);
+  }
+  return -1;
+}
+
+}  // namespace
+
+extern "C" int ev_host_run(const pxb_config* cfg, pxb_result* out, uint32_t* dig, pxb_acceptor_rec* acc,
+                           int64_t* totals, uint32_t* bail_ids, uint32_t* n_bail, uint64_t* micro_steps) {
+  if (!cfg || !eligible(cfg)) return -1;
+  return wheel_for(cfg->delay_max) == 8 ? run_w<8>(cfg, out, dig, acc, totals, bail_ids, n_bail, micro_steps)
+                                        : run_w<16>(cfg, out, dig, acc, totals, bail_ids, n_bail, micro_steps);
+}

@@ -1,0 +1,127 @@
+"""The per-lane kernel's state machine (csrc/paxos_ev.h), compiled for the HOST
+(tests/native/ev_host.cpp) and diffed against the CPU oracle instance by
+instance: results, log digests, final acceptor records and run totals.
+
+This checks the exact code the GPU runs (EvLane::init/step/finish) without a
+GPU; tests/test_gpu_parity.py then checks the device build end to end.
+Instances the kernel hands to the general kernel ("bailed": a FIFO, pool or
+ring capacity exceeded) are excluded here and must stay rare."""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle_c
+import pxb
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SRC = os.path.join(HERE, "native", "ev_host.cpp")
+OUT = os.path.join(HERE, "native", "_build", "libev_host.so")
+DEPS = [SRC] + [os.path.join(HERE, "..", "cloud-haskell-paxos_amd", "csrc", f)
+                for f in ("paxos_ev.h", "paxos_device.h")] + [os.path.join(HERE, "..", "include", "paxos_batch.h")]
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(OUT) or any(os.path.getmtime(d) > os.path.getmtime(OUT) for d in DEPS):
+            os.makedirs(os.path.dirname(OUT), exist_ok=True)
+            subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O2", "-std=c++17", "-fPIC",
+                            "-shared", "-o", OUT, SRC], check=True)
+        _lib = C.CDLL(OUT)
+    return _lib
+
+
+def ev_run(cfg, first, n):
+    N = cfg.n_acceptors
+    res = np.zeros((n, 4), np.uint32)
+    dig = np.zeros((n, N), np.uint32)
+    acc = np.zeros((n, N, 4), np.uint32)
+    tot = (C.c_int64 * 16)()
+    bail = np.zeros(max(n, 1), np.uint32)
+    nb, ms = C.c_uint32(0), C.c_uint64(0)
+    c = cfg.to_c(first, n)
+    p = lambda a: C.c_void_p(a.ctypes.data)  # noqa: E731
+    rc = lib().ev_host_run(C.byref(c), p(res), p(dig), p(acc), tot, p(bail), C.byref(nb), C.byref(ms))
+    assert rc == 0, "ev_host_run rc=%d" % rc
+    return res, dig, acc, pxb.counters_dict(list(tot)), bail[:nb.value].copy()
+
+
+def check(cfg, first, n, max_bail_frac=0.02):
+    res, dig, acc, cnt, bails = ev_run(cfg, first, n)
+    eres, edig, eacc, ecnt = oracle_c.run_cpu(cfg, first, n, threads=8, want_acceptors=True)
+    ok = np.ones(n, bool)
+    ok[bails] = False
+    bad = np.nonzero(((res != eres).any(1) | (dig != edig).any(1) | (acc != eacc).any((1, 2))) & ok)[0]
+    assert bad.size == 0, "instance %d: ev %s/%s oracle %s/%s" % (
+        first + bad[0], res[bad[0]], acc[bad[0]].tolist(), eres[bad[0]], eacc[bad[0]].tolist())
+    # totals: the oracle's minus the bailed instances' own
+    for b in bails:
+        _, _, _, bc = oracle_c.run_cpu(cfg, first + int(b), 1)
+        for k in ecnt:
+            ecnt[k] -= bc[k]
+    assert cnt == ecnt
+    assert len(bails) <= max_bail_frac * n + 1, "%d of %d instances bailed" % (len(bails), n)
+    return res, cnt, bails
+
+
+@pytest.mark.parametrize("c,n", [(3, 4000), (4, 3000), (5, 3000)])
+def test_baseline_configs(c, n):
+    _, cnt, bails = check(pxb.CONFIGS[c], 0, n)
+    if c in (3, 4):
+        assert len(bails) == 0
+
+
+@pytest.mark.parametrize("P", [1, 2, 3])
+@pytest.mark.parametrize("N", [2, 3, 4, 5, 6, 7, 8, 9])
+def test_topology_sweep(P, N):
+    cfg = pxb.Config(seed=0x1234 + 16 * P + N, n_proposers=P, n_acceptors=N, loss_ppm=150000,
+                     delay_max=5, skew_max=2, crash_ppm=150000, crash_len_max=8,
+                     crash_start_max=6, step_cap=200)
+    check(cfg, 1000, 1500)
+
+
+@pytest.mark.parametrize("kw", [
+    dict(loss_ppm=0, delay_max=15),
+    dict(loss_ppm=1000000),
+    dict(loss_ppm=500000, step_cap=1),
+    dict(crash_ppm=1000000, crash_len_max=1, crash_start_max=0),
+    dict(skew_max=4096, step_cap=4095),
+    dict(loss_ppm=350000, delay_max=15, step_cap=4095),
+    dict(delay_max=2, crash_ppm=400000, crash_len_max=4096, crash_start_max=65535),
+])
+def test_edge_schedules(kw):
+    base = dict(seed=99, n_proposers=2, n_acceptors=5)
+    base.update(kw)
+    check(pxb.Config(**base), 0, 1500, max_bail_frac=0.5)
+
+
+def test_instance_ids_cross_32bit():
+    check(pxb.CONFIGS[3], (1 << 32) - 1000, 2000)
+
+
+@pytest.mark.parametrize("i", range(24))
+def test_random_schedules(i):
+    rng = np.random.default_rng(0xE7 + i)
+    cfg = pxb.Config(
+        seed=int(rng.integers(0, 1 << 63)), n_proposers=int(rng.integers(1, 4)),
+        n_acceptors=int(rng.integers(2, 10)),
+        loss_ppm=int(rng.choice([0, rng.integers(1, 600000), 1000000])),
+        delay_max=int(rng.integers(2, 16)),
+        crash_ppm=int(rng.choice([0, rng.integers(1, 1000001)])),
+        crash_len_max=int(rng.integers(1, 40)), crash_start_max=int(rng.integers(0, 30)),
+        skew_max=int(rng.choice([0, rng.integers(1, 12)])),
+        step_cap=int(rng.choice([int(rng.integers(1, 64)), 256, 1024])),
+        randomize=bool(rng.random() < 0.3))
+    check(cfg, int(rng.integers(0, 1 << 34)), int(rng.integers(1, 800)), max_bail_frac=0.5)
+
+
+def test_bailed_instances_are_reported():
+    """Long delays with duelling proposers overflow the 4-slot physical FIFOs:
+    those instances are handed back (not silently wrong)."""
+    cfg = pxb.Config(seed=7, n_proposers=3, n_acceptors=9, delay_max=15, skew_max=0, step_cap=300)
+    _, _, bails = check(cfg, 0, 400, max_bail_frac=1.0)
+    assert len(bails) > 0
