@@ -2,84 +2,109 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2]
 
-One step = one launch of the batched Paxos kernel over one batch of fresh
-synthetic instances (BASELINE config 2 by default: 2^20 instances, 1 proposer,
-5 acceptors, no faults — the single-GPU configuration the metric is quoted
-on).  Instances are generated on the device from (seed, global instance id),
-so the inputs are resident before the timed region; outputs (16 B result +
-4 B/acceptor digest per instance) are written to HBM.  For N > 1 (torchrun,
-one process per GPU) each rank runs its own instance range (weak scaling, no
-data-path collective) and the run counters are summed with one RCCL
-all-reduce.  Prints ONE JSON line on rank 0.
+One step = one pxb_run_device call over one batch of fresh synthetic
+instances.  The headline workload is BASELINE config 2 (1 proposer, 5
+acceptors, no faults; the single-GPU configuration the metric is quoted on):
+a step runs 64 config-2 batches of 2^20 instances (2^26 fresh global ids), so
+the default 20 steps time well over 100 ms.  Instances are generated on the
+device from (seed, global instance id), so the inputs are resident before the
+timed region; outputs (16 B result + 4 B/acceptor digest per instance) are
+written to HBM.
+
+For N > 1 (one process per GPU, torchrun) each rank runs its own instance
+ranges (weak scaling, no data-path collective) and the run totals (decided
+counts, violation flags) are summed with one RCCL all-reduce.  `--gpus N`
+without torchrun spawns the N ranks itself (a child torch.distributed.run,
+started before this process touches a GPU).  Prints ONE JSON line on rank 0.
+
+The line also carries the north-star workload (BASELINE config 4: 64M
+instances with seeded crash windows, on this one GPU) with its own roofline,
+the other faulty configs at scale, and the CPU baseline (the oracle's C port
+on the host cores).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "cloud-haskell-paxos_amd"))
 
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
-
-import pxb  # noqa: E402
-
-HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-# HBM bytes per launch measured with rocprofv3 PMC passes (tools/profile_round.sh
-# + tools/traffic.py) for the default workload; rocprofv3 must wrap the process,
-# so bench.py reports the committed measurement of the same command.
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic_config2.json")
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
+# VALU issue peak: 256 CUs x 4 SIMDs, a wave64 VALU instruction every 2 cycles
+# per SIMD (MI355X_MICROARCH.md, "Wave scheduling") = 2 wave-instructions per
+# CU-cycle, at the 2.4 GHz peak engine clock
+CUS = 256
+VALU_PEAK_G = CUS * 2 * 2.4  # G wave64 VALU instructions / s (1228.8)
+PROFILES = os.path.join(ROOT, "profiles")
+BATCHES_PER_STEP = 64        # config-2 batches of 2^20 per timed step
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
-    ap.add_argument("--instances", type=int, default=0, help="per GPU per step (default: config size, capped)")
+    ap.add_argument("--instances", type=int, default=0, help="per GPU per step (default: the config's step size)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true")
     return ap.parse_args()
 
 
-def per_gpu_instances(c: int, world: int, override: int) -> int:
+def spawn_ranks(args) -> int:
+    """--gpus N outside torchrun: run N ranks as a child torch.distributed.run
+    (one process per GPU) and return its exit code.  Called before any GPU use."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def step_instances(c: int, override: int) -> int:
+    """Instances per GPU per step."""
+    import pxb
     if override:
         return override
-    n = pxb.CONFIG_INSTANCES[c]
-    if c == 4:
-        n //= 8                       # config 4 is quoted over 8 GPUs
-    if c == 5:
-        n //= 8
-    return max(1, n // (1 if c in (2, 3) else 1))
+    if c == 2:
+        return BATCHES_PER_STEP * pxb.CONFIG_INSTANCES[2]
+    if c in (4, 5):
+        return pxb.CONFIG_INSTANCES[c] // 8        # quoted over 8 GPUs: the per-GPU share
+    return pxb.CONFIG_INSTANCES[c]
 
 
-def run_workload(cfg, n, steps, warmup, rank, world, stream, dev):
-    """Returns (seconds for `steps` timed launches (max over ranks),
-    mean kernel ms, counters dict summed over ranks)."""
+def run_workload(cfg, n, steps, warmup, rank, world, stream, dev, warm_n=None):
+    """Times `steps` back-to-back pxb_run_device calls of n fresh instances.
+    Returns (wall seconds for the timed steps, max over ranks; mean ms per step
+    from HIP events on the launch stream; run totals summed over ranks)."""
+    import torch
+    import torch.distributed as dist
+    import pxb
     N = cfg.n_acceptors
     out = torch.empty((n, 4), dtype=torch.int32, device=dev)
     dig = torch.empty((n, N), dtype=torch.int32, device=dev)
     tot = torch.zeros(16, dtype=torch.int64, device=dev)
     sptr = stream.cuda_stream
 
-    def launch(step):
+    def launch(step, count):
         first = (step * world + rank) * n        # fresh global instance ids per step/rank
-        pxb.run_device(cfg, first, n, d_results=out, d_digests=dig, d_totals=tot, stream=sptr)
+        pxb.run_device(cfg, first, count, d_results=out, d_digests=dig, d_totals=tot, stream=sptr)
 
     with torch.cuda.stream(stream):
         for w in range(warmup):
-            launch(w)
+            launch(w, warm_n or n)
         stream.synchronize()
         tot.zero_()
-        # one event pair on the launch stream around the K back-to-back launches:
-        # (e1 - e0) / K is the average launch duration, inter-launch gaps
-        # included (no extra commands between the kernels)
+        # one event pair on the launch stream around the K back-to-back steps:
+        # (e1 - e0) / K is the mean step time, gaps between kernels included
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         if world > 1:
             dist.barrier()
@@ -87,7 +112,7 @@ def run_workload(cfg, n, steps, warmup, rank, world, stream, dev):
         t0 = time.perf_counter()
         e0.record(stream)
         for k in range(steps):
-            launch(warmup + k)
+            launch(warmup + k, n)
         e1.record(stream)
         torch.cuda.synchronize()
         if world > 1:
@@ -103,17 +128,45 @@ def run_workload(cfg, n, steps, warmup, rank, world, stream, dev):
     return float(elapsed.item()), kms, pxb.counters_dict(tot.cpu().tolist())
 
 
-def traffic_per_launch(c, n):
-    """PMC-measured HBM bytes per launch (FETCH_SIZE x2 + WRITE_SIZE) from the
-    committed profile of this exact workload, else None."""
+def step_profile(workload: str, n: int):
+    """The committed rocprofv3 profile of this workload (tools/profile_round.sh
+    + tools/step_profile.py): PMC counts per step, or None."""
+    path = os.path.join(PROFILES, "r02_%s_step.json" % workload)
     try:
-        with open(TRAFFIC_FILE) as f:
-            t = json.load(f)
+        with open(path) as f:
+            p = json.load(f)
     except (OSError, ValueError):
-        return None
-    if t.get("config") != c or t.get("instances") != n:
-        return None
-    return t.get("bytes_per_launch")
+        return None, path
+    return (p if p.get("instances_per_step") == n else None), path
+
+
+def roofline(workload, n, kms, canon_bytes_per_step):
+    """VALU-issue roofline of one step: the PMC-counted VALU wave-instructions
+    of the step's kernels (committed profile of this workload) over the step
+    time measured now; HBM bytes from the same profile's FETCH/WRITE passes."""
+    prof, path = step_profile(workload, n)
+    canon_gbs = canon_bytes_per_step / (kms * 1e-3) / 1e9
+    r = {"bound": "valu_issue", "unit": "G VALU wave-instructions/s", "peak": VALU_PEAK_G,
+         "achieved": None, "frac": None, "traffic": None,
+         "peak_basis": "256 CUs x 2 wave64 VALU instructions per CU-cycle x 2.4 GHz (MI355X_MICROARCH.md)",
+         "canonical_equiv_GBps": canon_gbs,
+         "canonical_note": "SURVEY.md 8(d) canonical bytes / step time: the traffic of a design whose "
+                           "SoA state round-trips HBM every step; this engine keeps it on chip, so this "
+                           "is not a bandwidth measurement",
+         "physical_GBps": None, "physical_frac": None, "profile": os.path.relpath(path, ROOT)}
+    if prof:
+        valu = prof["valu_insts_per_step"]
+        r["achieved"] = valu / (kms * 1e-3) / 1e9
+        r["frac"] = r["achieved"] / VALU_PEAK_G
+        r["valu_insts_per_step"] = valu
+        r["dominant_kernel"] = prof.get("dominant_kernel")
+        r["dominant_share_of_step"] = prof.get("dominant_share")
+        hbm = prof.get("hbm_bytes_per_step")
+        if hbm is not None:
+            r["traffic"] = hbm
+            r["physical_GBps"] = hbm / (kms * 1e-3) / 1e9
+            r["physical_frac"] = r["physical_GBps"] / HBM_PEAK_GBS
+    return r
 
 
 def wire_bench(stream, dev, n=1 << 24, reps=5):
@@ -124,6 +177,8 @@ def wire_bench(stream, dev, n=1 << 24, reps=5):
     8 (offset) + record; decode record + 16 offset reads + 16 (pxb_msg) + 4
     (status)."""
     import numpy as np
+    import torch
+    import pxb
     rng = np.random.default_rng(0)
     kind = rng.choice([0, 0, 1, 2], size=n).astype(np.uint32)
     msgs = np.zeros((n, 4), np.uint32)
@@ -137,16 +192,13 @@ def wire_bench(stream, dev, n=1 << 24, reps=5):
     d_b = torch.zeros(n * pxb.WIRE_MAX_BYTES, dtype=torch.uint8, device=dev)
     d_back = torch.zeros_like(d_m)
     d_st = torch.zeros(n, dtype=torch.int32, device=dev)
-    lib = pxb.load()
     sp = stream.cuda_stream
-    ptr = lambda t: pxb.C.c_void_p(t.data_ptr())  # noqa: E731
 
     def enc():   # fused size + encode (pxb_wire_encode_all)
         pxb.wire_encode_device(d_m, pxb.WIRE_RESPONSE, d_o, d_b, stream=sp)
 
     def dec():
-        pxb.check(lib.pxb_wire_decode(ptr(d_b), ptr(d_o), n, pxb.WIRE_RESPONSE, ptr(d_back), ptr(d_st),
-                                      pxb.C.c_void_p(sp)))
+        pxb.wire_decode_device(d_b, d_o, n, pxb.WIRE_RESPONSE, d_back, d_st, stream=sp)
 
     out = {"messages": n}
     with torch.cuda.stream(stream):
@@ -167,10 +219,26 @@ def wire_bench(stream, dev, n=1 << 24, reps=5):
     return out
 
 
+def host_cores():
+    """CPUs this process may run on, and the cgroup CPU quota if one is set."""
+    n = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    return n, quota
+
+
 def cpu_baseline(cfg, budget_s):
+    """The oracle's C port (oracle/paxos_oracle.c) on every host core the
+    process may use (nproc), on a bounded sample of the same config (ids from
+    2^40), then on one core."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_c                          # CPU restatement (oracle/), baseline only
-    threads = min(16, os.cpu_count() or 1)
+    threads, quota = host_cores()
     chunk = 1 << 17
     done, first = 0, 1 << 40
     t0 = time.perf_counter()
@@ -180,23 +248,42 @@ def cpu_baseline(cfg, budget_s):
         if time.perf_counter() - t0 >= budget_s:
             break
     dt = time.perf_counter() - t0
-    # the same port on one core (all host cores and 1 core)
     one, t1 = 0, time.perf_counter()
     while time.perf_counter() - t1 < min(3.0, budget_s):
         oracle_c.run_cpu(cfg, first + done + one, 1 << 14, threads=1)
         one += 1 << 14
     dt1 = time.perf_counter() - t1
     return {"value": done / dt, "unit": "instances/s", "cores": threads, "kind": "port",
+            "nproc": os.cpu_count(), "cgroup_cpu_quota": quota,
             "sample": "%d instances of the same config (ids from 2^40), oracle/paxos_oracle.c "
-                      "on %d host threads, %.1f s" % (done, threads, dt),
+                      "on %d host threads (all CPUs in the process affinity), %.1f s" % (done, threads, dt),
             "one_core": {"value": one / dt1, "sample": "%d further instances, 1 thread, %.1f s" % (one, dt1)}}
+
+
+def faulty_line(name, c, n, steps, warmup, stream, dev, warm_n):
+    import pxb
+    es, ek, ecnt = run_workload(pxb.CONFIGS[c], n, steps, warmup, 0, 1, stream, dev, warm_n=warm_n)
+    line = {"workload": name, "instances_per_step": n, "instances_per_s": ecnt["instances"] / es,
+            "decided_per_s": ecnt["decided"] / es, "ms_per_step": es / steps * 1e3, "kernel_ms": ek,
+            "mean_steps_per_instance": ecnt["steps"] / max(1, ecnt["instances"]),
+            "roofline": roofline("config%d" % c, n, ek, ecnt["canon_bytes"] / steps), "counters": ecnt}
+    assert ecnt["instances"] == n * steps, ecnt
+    assert ecnt["decided"] + ecnt["undecided"] == ecnt["instances"]
+    return line
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.exit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    import pxb
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
@@ -204,7 +291,7 @@ def main():
     stream = torch.cuda.Stream(dev)
     c = args.config
     cfg = pxb.CONFIGS[c]
-    n = per_gpu_instances(c, world, args.instances)
+    n = step_instances(c, args.instances)
 
     secs, kms, cnt = run_workload(cfg, n, args.steps, args.warmup, rank, world, stream, dev)
     total_inst = n * world * args.steps
@@ -212,10 +299,6 @@ def main():
     if c == 2:   # closed forms of the fault-free config: every instance decides
         assert cnt["decided"] == total_inst and cnt["canon_bytes"] == 1140 * total_inst, cnt
     value = cnt["decided"] / secs                         # decided instances / s, whole job
-    canon_per_launch = cnt["canon_bytes"] / (args.steps * world)
-    achieved = canon_per_launch / (kms * 1e-3) / 1e9      # GB/s, per-GPU kernel
-    traffic = traffic_per_launch(c, n)                    # PMC-measured HBM bytes per launch
-    phys = None if traffic is None else traffic / (kms * 1e-3) / 1e9
     line = {
         "metric": "Paxos instances decided/sec (node)",
         "value": value,
@@ -229,35 +312,28 @@ def main():
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic (Philox4x32-10 schedule from seed + global instance id)",
-        "config": {"workload": "BASELINE config %d" % c, "instances_per_gpu_per_step": n,
+        "config": {"workload": "BASELINE config %d" % c + (
+                       ": %d batches of 2^20 instances per step" % (n >> 20) if c == 2 else ""),
+                   "instances_per_gpu_per_step": n,
                    "proposers": cfg.n_proposers, "acceptors": cfg.n_acceptors,
                    "loss_ppm": cfg.loss_ppm, "delay_max": cfg.delay_max, "skew_max": cfg.skew_max,
                    "crash_ppm": cfg.crash_ppm, "step_cap": cfg.step_cap,
                    "randomize": cfg.randomize, "seed": hex(cfg.seed),
-                   "parallelism": "instance-range shards x%d" % world},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "accounting": "SURVEY.md 8(d) canonical bytes (%.0f B/instance), "
-                                   "avg %.4f ms/launch (batch + finalize kernels, HIP events)" % (
-                                       cnt["canon_bytes"] / max(1, cnt["instances"]), kms),
-                     # the canonical count is the traffic of a design whose SoA state
-                     # round-trips HBM every step; this kernel keeps the state on chip,
-                     # so it can exceed the HBM peak.  What HBM really carries:
-                     "physical_GBps": phys, "physical_frac": None if phys is None else phys / HBM_PEAK_GBS,
-                     "limiter": "VALU issue (per-step protocol logic on chip; profiles/*_pmc_valu*)"},
+                   "parallelism": "instance-range shards x%d" % world, "rccl_world": world},
+        "roofline": roofline("config%d" % c, n, kms, cnt["canon_bytes"] / (args.steps * world)),
         "counters": cnt,
     }
     if rank == 0 and not args.no_extra and c == 2 and world == 1:
+        # the north star: BASELINE config 4 (64M instances, 2 duelling proposers,
+        # 7 acceptors, seeded crash windows) all on this one GPU
+        line["north_star"] = faulty_line("BASELINE config 4: 2^26 instances on 1 GPU", 4,
+                                         pxb.CONFIG_INSTANCES[4], 1, 1, stream, dev, 1 << 22)
         extra = {}
-        # faulty configs: 3 (2^24, duelling + loss), 4 (the north-star 64M instances
-        # with seeded crash windows, all on this one GPU), 5 (fuzz, 2^22 of 2^28)
-        for ec, en, ek_steps in ((3, pxb.CONFIG_INSTANCES[3], 2), (4, pxb.CONFIG_INSTANCES[4], 1), (5, 1 << 22, 2)):
-            es, ek, ecnt = run_workload(pxb.CONFIGS[ec], en, ek_steps, 1, 0, 1, stream, dev)
-            canon_gbs = ecnt["canon_bytes"] / ek_steps / (ek * 1e-3) / 1e9
-            extra["config%d" % ec] = {"instances_per_step": en, "instances_per_s": ecnt["instances"] / es,
-                                      "decided_per_s": ecnt["decided"] / es, "kernel_ms": ek,
-                                      "canonical_GBps": canon_gbs, "canonical_frac": canon_gbs / HBM_PEAK_GBS,
-                                      "counters": ecnt}
+        extra["config3"] = faulty_line("BASELINE config 3: 2^24 instances", 3, pxb.CONFIG_INSTANCES[3],
+                                       2, 1, stream, dev, 1 << 22)
+        extra["config5"] = faulty_line("BASELINE config 5: 2^25 instances (the per-GPU share of 2^28 "
+                                       "over 8 GPUs)", 5, pxb.CONFIG_INSTANCES[5] // 8, 1, 1, stream, dev,
+                                       1 << 22)
         extra["wire_codec"] = wire_bench(stream, dev)
         # log mode: stock Main.hs topology with the ticker running (SEMANTICS §9)
         en = 1 << 20
@@ -268,6 +344,8 @@ def main():
         line["extra"] = extra
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
+        if "north_star" in line:
+            line["north_star"]["cpu_baseline"] = cpu_baseline(pxb.CONFIGS[4], min(args.cpu_seconds, 8.0))
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -46,6 +46,7 @@ constexpr int QD = PXB_QUEUE_DEPTH;   // 8: ring slots per directed link
 constexpr int LT = PXB_LOG_TRACK;
 static_assert(QD == 8, "due-nibble word and ring masks assume 8 slots");
 static_assert(PXB_MAX_STEP_CAP <= 8192, "14-bit packed tickets / steps");
+static_assert(PXB_TICKET_LIMIT <= (1 << 14), "the overflow flag must fire before a 14-bit ticket field wraps");
 #ifndef PXB_OCC_P1
 #define PXB_OCC_P1 4
 #endif

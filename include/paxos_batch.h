@@ -44,7 +44,7 @@ extern "C" {
 #define PXB_MAX_STEP_CAP 8192
 #define PXB_QUEUE_DEPTH     8    /* messages per directed link              */
 #define PXB_LOG_TRACK      32    /* log positions checked for divergence    */
-#define PXB_TICKET_LIMIT (1 << 15)
+#define PXB_TICKET_LIMIT (1 << 14)   /* = the 14-bit ticket fields of the kernel words */
 #define PXB_MAX_TICKS    4096    /* log mode: Ticks per proposer            */
 
 /* pxb_config.flags */

@@ -112,7 +112,7 @@ F_QUEUE_OVERFLOW = 1 << 5
 F_TICKET_OVERFLOW = 1 << 6
 F_LOG_TRUNC = 1 << 7
 
-TICKET_LIMIT = 1 << 15      # tickets at/above this set F_TICKET_OVERFLOW
+TICKET_LIMIT = 1 << 14      # tickets at/above this set F_TICKET_OVERFLOW (14-bit kernel fields)
 QUEUE_DEPTH = 8             # per directed link (docs/SEMANTICS.md §3)
 LOG_TRACK = 32              # log positions checked for divergence
 
@@ -454,7 +454,7 @@ class _Link:
 
 
 def run_instance(cfg: Config, inst: int, queue_depth: int = QUEUE_DEPTH,
-                 log_track: int = LOG_TRACK) -> InstanceResult:
+                 log_track: int = LOG_TRACK, ticket_limit: int = TICKET_LIMIT) -> InstanceResult:
     """Run one instance under the canonical step schedule (docs/SEMANTICS.md)."""
     N = cfg.n_acceptors
     prm = instance_params(cfg, inst)
@@ -559,7 +559,7 @@ def run_instance(cfg: Config, inst: int, queue_depth: int = QUEUE_DEPTH,
                     bcast(p, s, proposer_handle(pr, N, kind, x, y, z))
             if active:
                 canon += 48
-            if pr.ticket >= TICKET_LIMIT:
+            if pr.ticket >= ticket_limit:
                 flags |= F_TICKET_OVERFLOW
         # -- quiescence
         in_flight = any(l.q for row in req for l in row) or any(l.q for row in rsp for l in row)

@@ -251,3 +251,23 @@ def test_c_handlers_match_python_random():
         exp_rep = [pxb.MSG_NONE, 0, 0, 0] if r is None else list(r)
         assert list(rep[i]) == exp_rep
         assert list(st2[i]) == [a.t_max, a.t_store, a.val, len(a.log) | (int(a.dead) << 31)]
+
+
+def test_ticket_limit_matches_kernel_packing():
+    """The kernel packs tickets into 14-bit fields; TICKET_OVERFLOW must fire
+    at 2^14 in the header, the C oracle (via the header) and the Python oracle."""
+    import re
+    hdr = open(os.path.join(os.path.dirname(__file__), "..", "include", "paxos_batch.h")).read()
+    assert re.search(r"#define PXB_TICKET_LIMIT \(1 << 14\)", hdr)
+    assert R.TICKET_LIMIT == 1 << 14
+
+
+def test_ticket_at_the_limit_sets_the_flag():
+    """A duel drives tickets up; with the limit lowered to a reachable value the
+    flag is set exactly when some proposer's ticket reaches it (a proposer's
+    ticket never decreases, so its final value is its maximum)."""
+    cfg = R.Config(seed=5, n_proposers=2, n_acceptors=3, delay_max=3, step_cap=60)
+    for inst in range(40):
+        top = max(p.ticket for p in R.run_instance(cfg, inst).proposers)
+        assert R.run_instance(cfg, inst, ticket_limit=top).flags & R.F_TICKET_OVERFLOW
+        assert not R.run_instance(cfg, inst, ticket_limit=top + 1).flags & R.F_TICKET_OVERFLOW
