@@ -2,43 +2,47 @@
 // single-decree schedules (loss, delay, crash windows, duelling, fuzzing).
 //
 // One lane runs one whole instance: its N acceptors (Server.hs:44-89), its P
-// proposers (Client.hs:85-207) and its 2·P·N directed links.  The reference's
-// actors are replaced by a per-lane state machine that, every wave iteration,
-// performs ONE micro-step of its own instance in canonical order
-// (docs/SEMANTICS.md §6):
+// proposers (Client.hs:85-207) and its 2·P·N directed links.  Within a step
+// the acceptor phase and the proposer phase are independent (every send is
+// due one step later at the earliest, docs/SEMANTICS.md §6), so every wave
+// iteration a lane does, predicated and without branches:
 //
-//   ACC   one request handled by one acceptor (handleClientRequest,
-//         Server.hs:51-78) + its reply sent on link a -> p;
-//   PROP  one Tick (handleTick, Client.hs:196-207) or one response folded
-//         by one proposer (handleServerResponse, Client.hs:125-189), and the
-//         next copy of a pending broadcast (sendToAllServers,
-//         Client.hs:122-123) sent on link p -> a;
-//   ADV   end of step: quiescence / step cap (the role of Main.hs:49-53),
-//         then the next step's due links from a timing wheel.
+//   ACC   one due request handled by one acceptor (handleClientRequest,
+//         Server.hs:51-78) and its reply sent on link a -> p;
+//   COPY  the next copy of a pending broadcast sent on link p -> a
+//         (sendToAllServers, Client.hs:122-123);
+//   PROP  one input of one proposer: its Tick (handleTick, Client.hs:196-207)
+//         or one due response (handleServerResponse, Client.hs:125-189),
+//         whose broadcasts join the pending queue;
+//   END   when the step has no work left: quiescence / step cap (the role of
+//         Main.hs:49-53), then the next step that has a due message or a Tick
+//         (steps without either change nothing and are skipped).
+//
+// The canonical order (§6) only constrains each process: acceptor a takes
+// its requests by (p, seq), proposer p its Tick and then its responses by
+// (a, seq).  The due-request mask has bit a*PM+p, so its lowest set bit
+// serves each acceptor in proposer order; the proposer-input mask has bit
+// p*(N+1) for the Tick and p*(N+1)+1+a for link a -> p.
 //
 // Lanes are independent (instances share nothing: Main.hs:41-45), so a wave
 // never waits on its slowest instance: a lane whose instance ends writes its
-// outputs and takes the next instance from the work queue.  Every lane sends
-// at most one message per micro-step, so the wave issues one Philox4x32-10
-// draw per iteration for all 64 lanes.
+// outputs and takes the next instance from the work queue.
 //
-// Per-lane state (LDS words are lane-interleaved, [word][lane]: every access
-// is bank-conflict free):
-//   registers  proposer states, pending-broadcast queue, link-free masks,
-//              counters;
-//   LDS        request-link FIFOs (4 x {broadcast slot, due} per link, the
-//              payload lives once per broadcast in a per-proposer ring),
-//              response-link FIFOs (indices into a per-lane pool of response
-//              words), the reply sequence numbers, acceptor states and
-//              digests, isolation windows, and a timing wheel of per-step
-//              due-link masks.
+// Per-lane state:
+//   registers  proposer states, acceptor words (T_max, T_store, val, dead,
+//              log length) and isolation windows, pending-broadcast queue,
+//              ring reference counts, due masks, counters;
+//   LDS        (lane-interleaved words, [word][lane]: every access is
+//              bank-conflict free) request-link FIFOs (4 x {broadcast ring
+//              slot, due} per link; the payload lives once per broadcast in a
+//              per-proposer ring), response-link FIFOs (indices into a
+//              per-lane pool of response words), reply sequence numbers, log
+//              digests, and a timing wheel of per-step due-link masks.
 //
 // The semantic queue depth stays PXB_QUEUE_DEPTH = 8; the physical FIFOs hold
 // 4 (and the pool POOL responses).  An instance that would need more is
 // "bailed": its id goes to a list that the general kernel (paxos_kernel.h)
-// re-runs from scratch, so results stay exact for every schedule.  Measured
-// on the BASELINE configs (tools/ study): config 4 never
-// bails, config 5 bails ~0.3 % of instances.
+// re-runs from scratch, so results stay exact for every schedule.
 //
 // This file is plain C++ over a memory accessor, so the same code runs on the
 // device (LDS accessor) and in the host unit test (tests/test_ev_host.py),
@@ -62,44 +66,46 @@ constexpr uint32_t MAX_STEP_CAP = 4095;   // 12-bit tickets (tickets <= step_cap
 static_assert(MAX_STEP_CAP < PXB_TICKET_LIMIT, "EV tickets never reach the overflow limit");
 
 // lane modes
-constexpr uint32_t M_IDLE = 0, M_ACC = 1, M_PROP = 2;
+constexpr uint32_t M_IDLE = 0, M_RUN = 1;
 
 template <int PM_, int N_, int POOL_, int W_>
 struct Shape {
   static constexpr int PM = PM_, N = N_, POOL = POOL_, W = W_;
-  static constexpr int NL = PM * N;                  // links per direction
+  static constexpr int NLQ = PM * N;                 // request (and response) links
+  static constexpr int NIN = PM * (N + 1);           // proposer-input bits (Tick + N links each)
+  static constexpr int WW = (NLQ + NIN <= 32) ? 1 : 2;   // wheel words per slot
+  static constexpr int ISH = (WW == 1) ? NLQ : 0;    // input-bit offset in its wheel word
   static constexpr int IB = POOL <= 32 ? 5 : 6;      // pool index bits
-  static constexpr int WW = (NL <= 16) ? 1 : 2;      // wheel words per slot
-  static constexpr int PSH = (WW == 1) ? 16 : 0;     // proposer-link bit offset in the wheel word
   // LDS word offsets
-  static constexpr int REQM = 0;                     // NL: request links, index a*PM + p
-  static constexpr int RSPM = REQM + NL;             // NL: response links, index p*N + a
-  static constexpr int RSEQ = RSPM + NL;             // NL halfwords: reply seq, index a*PM + p
-  static constexpr int POOLW = RSEQ + (NL + 1) / 2;  // POOL response words
+  static constexpr int REQ = 0;                      // NLQ: request links, index a*PM + p
+  static constexpr int RSP = REQ + NLQ;              // NLQ: response links, index p*N + a
+  static constexpr int RSEQ = RSP + NLQ;             // NLQ halfwords: reply seq, index a*PM + p
+  static constexpr int POOLW = RSEQ + (NLQ + 1) / 2; // POOL response words
   static constexpr int BRING = POOLW + POOL;         // PM*BR halfwords: broadcast payloads
-  static constexpr int ACCW = BRING + PM * BR / 2;   // N acceptor words
-  static constexpr int ACCD = ACCW + N;              // N digests
-  static constexpr int ACCC = ACCD + N;              // N isolation windows
-  static constexpr int WHEEL = ACCC + N;             // W * WW due-link masks
+  static constexpr int ACCD = BRING + PM * BR / 2;   // N digests
+  static constexpr int WHEEL = ACCD + N;             // W * WW due masks
   static constexpr int WORDS = WHEEL + W * WW;
   static_assert(W == 8 || W == 16, "wheel of 8 or 16 steps");
-  static_assert(NL <= 32, "link masks are 32-bit");
+  static_assert(NIN <= 32 && NLQ <= 32, "masks are 32-bit");
   static_assert(4 * IB + 7 <= 32, "response-link word");
 };
 
 // Layouts (docs/SEMANTICS.md §2 encodings; tickets < 2^12):
 //   request-link word   entry i (7 bits at 7i): broadcast slot [2:0] | due&15 [6:3];  len [30:28]
 //   response-link word  pool index i (IB bits at IB*i); len [4IB+2:4IB]; last due&15 [4IB+6:4IB+3]
-//   response word       x [11:0] | y [23:12] | z [25:24] | due&15 [29:26] | kind [31:30]
+//   response word       x [11:0] | y [23:12] | z [25:24] | kind [31:30]
 //   broadcast payload   x [11:0] | z [13:12] | kind [15:14]
 //   acceptor word       t_max [11:0] | t_store [23:12] | val [25:24] | dead [26] | log_len [31:27]
 //   window              c0 [15:0] | c1 [31:16]  (clamped to 4096: steps are < 4095)
+// The due step of a queued response is kept in its link word only for the
+// tail (the FIFO max-chain of §5); "is the next one due now" reads the
+// response's own due nibble [29:26] (x, y < 2^12, z < 4: bits 26..29 free).
 
 // Per-launch parameters shared by the device kernel and the host test.
 struct EvParams {
   uint64_t first_instance;
   uint32_t k0, k1;
-  uint32_t cfg;                       // CFG_* bits (paxos_kernel.h)
+  uint32_t cfg;                       // EV_CFG_* bits
   uint32_t n_prop, delay_max;
   uint32_t loss_m1, crash_m1;
   uint32_t loss_ppm, crash_ppm;
@@ -112,6 +118,7 @@ __host__ __device__ inline uint64_t ev_threshold(uint32_t ppm) {
 }
 
 __host__ __device__ __forceinline__ uint32_t ctz32(uint32_t x) { return x ? (uint32_t)__builtin_ctz(x) : 32u; }
+__host__ __device__ __forceinline__ uint32_t popc32(uint32_t x) { return (uint32_t)__builtin_popcount(x); }
 
 // Per-instance outcome handed to the driver when a lane finishes.
 struct EvOut {
@@ -120,11 +127,19 @@ struct EvOut {
   uint32_t steps;
 };
 
+#ifndef PXB_EV_CPRE
+#define PXB_EV_CPRE 1
+#endif
+#ifndef PXB_EV_CPOST
+#define PXB_EV_CPOST 1
+#endif
+
 template <int PM, int N, int POOL, int W, class Mem>
 struct EvLane {
   using S = Shape<PM, N, POOL, W>;
   using pool_mask_t = typename std::conditional<(POOL > 32), unsigned long long, uint32_t>::type;
-  static constexpr uint32_t NL = S::NL;
+  static constexpr uint32_t NLQ = S::NLQ;
+  static constexpr uint32_t WM = (uint32_t)W - 1u;
 
   Mem m;
   // ---- instance ----
@@ -132,16 +147,20 @@ struct EvLane {
   uint32_t gid;                       // instance index within the launch
   uint32_t lo, hi;                    // global instance id (Philox counter words 0, 1)
   uint32_t P, dmax, loss_m1;
-  bool lossy, faulty;
+  bool lossy, faulty, crashy;
   int32_t s, last_tick;
-  uint32_t acc_mask, prop_mask;       // this step's links with due messages left
-  uint32_t tickp, stepped, pcur;      // Ticks due this step, proposers with input, proposer in turn
+  uint32_t acc_mask;                  // this step's request links with due messages left
+  uint32_t in_mask;                   // this step's proposer inputs left (Tick / response links)
+  uint32_t occ;                       // wheel slots holding due bits
+  uint32_t iso;                       // acceptors isolated at step s
   // proposer states (ClientState, Client.hs:58-67): tickets < 2^12, commands = clientId
   uint32_t ticket[PM], cmd[PM], acks[PM], rs[PM], mr_t[PM], mr_v[PM], r2_v[PM], pending[PM];
   uint32_t skew[PM];
   uint32_t nsent[PM];                 // broadcasts of p whose copies have started (request-link seq)
   uint32_t bnext[PM];                 // next broadcast-ring slot
   uint32_t refc[PM];                  // ring-slot reference counts (4-bit nibbles)
+  // acceptor states (Server.hs:24-31) and isolation windows
+  uint32_t accw[N], win[N];
   uint32_t pq, pq_len, acur;          // pending broadcasts (p << 3 | slot, 5 bits each), next acceptor
   pool_mask_t pfree;                  // free response-pool words
   uint32_t in_flight;
@@ -155,20 +174,76 @@ struct EvLane {
                                                    : (pool_mask_t)(((pool_mask_t)1 << (POOL % (8 * sizeof(pool_mask_t)))) - 1u);
   }
 
-  // ---- helpers over the per-proposer register arrays (q may differ per lane) ----
-  __host__ __device__ static uint32_t getp(const uint32_t (&v)[PM], uint32_t q) {
-    uint32_t r = v[0];
+  // ---- selects over per-proposer / per-acceptor register arrays (index may differ per lane) ----
+  // The operands go through an empty asm: otherwise LLVM folds the select
+  // chain into one load at a selected offset, and the dynamic offset keeps
+  // the whole lane state in scratch memory instead of VGPRs.
+  __host__ __device__ static __forceinline__ uint32_t opaque(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __asm__("" : "+v"(x));
+#endif
+    return x;
+  }
+  template <int K>
+  __host__ __device__ static __forceinline__ uint32_t get(const uint32_t (&v)[K], uint32_t q) {
+    uint32_t r = opaque(v[0]);
 #pragma unroll
-    for (int i = 1; i < PM; ++i) r = (q == (uint32_t)i) ? v[i] : r;
+    for (int i = 1; i < K; ++i) r = (q == (uint32_t)i) ? opaque(v[i]) : r;
     return r;
   }
-  __host__ __device__ static void setp(uint32_t (&v)[PM], uint32_t q, uint32_t x) {
+  template <int K>
+  __host__ __device__ static __forceinline__ void set(uint32_t (&v)[K], uint32_t q, uint32_t x, bool pred) {
 #pragma unroll
-    for (int i = 0; i < PM; ++i) v[i] = (q == (uint32_t)i) ? x : v[i];
+    for (int i = 0; i < K; ++i) v[i] = (pred && q == (uint32_t)i) ? x : v[i];
+  }
+
+  __host__ __device__ __forceinline__ uint32_t iso_at(int32_t t) const {
+    uint32_t r = 0u;
+#pragma unroll
+    for (int a = 0; a < N; ++a) {
+      const uint32_t c0 = win[a] & 0xFFFFu, c1 = win[a] >> 16;
+      r |= (c0 <= (uint32_t)t && (uint32_t)t < c1) ? (1u << a) : 0u;
+    }
+    return r;
+  }
+
+  // the Tick bits of step t
+  __host__ __device__ __forceinline__ uint32_t ticks_at(int32_t t) const {
+    uint32_t r = 0u;
+#pragma unroll
+    for (int p = 0; p < PM; ++p) r |= ((uint32_t)p < P && skew[p] == (uint32_t)t) ? (1u << (p * (N + 1))) : 0u;
+    return r;
+  }
+
+  // enter step t: its due links from the wheel, its Ticks, its isolated acceptors;
+  // 48 canonical bytes per proposer with an input (SEMANTICS §8)
+  __host__ __device__ __forceinline__ void enter(int32_t t) {
+    s = t;
+    const uint32_t slot = (uint32_t)t & WM;
+    uint32_t wq, wi;
+    if (S::WW == 1) {
+      const uint32_t wv = m.ld(S::WHEEL + slot);
+      wq = wv & ((1u << NLQ) - 1u);
+      wi = wv >> S::ISH;
+    } else {
+      wq = m.ld(S::WHEEL + 2u * slot);
+      wi = m.ld(S::WHEEL + 2u * slot + 1u);
+      m.st(S::WHEEL + 2u * slot + 1u, 0u);
+    }
+    m.st(S::WHEEL + S::WW * slot, 0u);
+    occ &= ~(1u << slot);
+    acc_mask = wq;
+    in_mask = wi | ticks_at(t);
+#pragma unroll
+    for (int p = 0; p < PM; ++p) {
+      const uint32_t grp = ((1u << (N + 1)) - 1u) << (p * (N + 1));
+      canon += (in_mask & grp) ? 48u : 0u;
+    }
+    if (crashy) iso = iso_at(t);
   }
 
   // ---- instance start: parameters, Tick skews, isolation windows (SEMANTICS §4) ----
-  __host__ __device__ void init(const EvParams& kp, uint32_t g) {
+  __host__ __device__ __forceinline__ void init(const EvParams& kp, uint32_t g) {
     gid = g;
     const uint64_t inst = kp.first_instance + g;
     lo = (uint32_t)inst;
@@ -176,7 +251,7 @@ struct EvLane {
     P = kp.n_prop;
     dmax = kp.delay_max;
     lossy = (kp.cfg & EV_CFG_LOSSY) != 0u;
-    bool crashy = (kp.cfg & EV_CFG_CRASHY) != 0u;
+    crashy = (kp.cfg & EV_CFG_CRASHY) != 0u;
     loss_m1 = kp.loss_m1;
     uint32_t crash_m1 = kp.crash_m1;
     if (kp.cfg & EV_CFG_RANDOMIZE) {                  // config-5 fuzz (SEMANTICS §4)
@@ -194,19 +269,16 @@ struct EvLane {
     uint4 wsk = make_uint4(0, 0, 0, 0);
     if (kp.skew_max > 0u) wsk = philox(lo, hi, 0u, 2u << 24, kp.k0, kp.k1);
     last_tick = 0;
-    tickp = 0;
 #pragma unroll
     for (int p = 0; p < PM; ++p) {
       const uint32_t wp = (p == 0) ? wsk.x : (p == 1) ? wsk.y : wsk.z;
       skew[p] = (kp.skew_max > 0u) ? mulhi_n(wp, kp.skew_max + 1u) : 0u;
-      if ((uint32_t)p < P) {
-        last_tick = ((int32_t)skew[p] > last_tick) ? (int32_t)skew[p] : last_tick;
-        tickp |= (skew[p] == 0u) ? (1u << p) : 0u;
-      }
+      if ((uint32_t)p < P) last_tick = ((int32_t)skew[p] > last_tick) ? (int32_t)skew[p] : last_tick;
       ticket[p] = cmd[p] = acks[p] = mr_t[p] = mr_v[p] = r2_v[p] = pending[p] = 0u;
       rs[p] = IDLE;
       nsent[p] = bnext[p] = refc[p] = 0u;
     }
+    bool anyiso = false;
 #pragma unroll
     for (int a = 0; a < N; ++a) {
       uint32_t c0 = 0, c1 = 0;
@@ -219,17 +291,19 @@ struct EvLane {
       }
       c0 = c0 < 4096u ? c0 : 4096u;
       c1 = c1 < 4096u ? c1 : 4096u;
-      m.st(S::ACCW + a, 0u);
+      anyiso = anyiso || c1 > c0;
+      win[a] = c0 | (c1 << 16);
+      accw[a] = 0u;
       m.st(S::ACCD + a, 0x811C9DC5u);
-      m.st(S::ACCC + a, c0 | (c1 << 16));
+    }
+    crashy = anyiso;                                 // no window at all: skip the isolation test
+#pragma unroll
+    for (int L = 0; L < (int)NLQ; ++L) {
+      m.st(S::REQ + L, 0u);
+      m.st(S::RSP + L, 0u);
     }
 #pragma unroll
-    for (int L = 0; L < (int)NL; ++L) {
-      m.st(S::REQM + L, 0u);
-      m.st(S::RSPM + L, 0u);
-    }
-#pragma unroll
-    for (int i = 0; i < ((int)NL + 1) / 2; ++i) m.st(S::RSEQ + i, 0u);
+    for (int i = 0; i < ((int)NLQ + 1) / 2; ++i) m.st(S::RSEQ + i, 0u);
 #pragma unroll
     for (int i = 0; i < W * S::WW; ++i) m.st(S::WHEEL + i, 0u);
     pq = pq_len = acur = 0u;
@@ -238,333 +312,263 @@ struct EvLane {
     lflags = rounds = dval = dtick = execs = msgs = canon = 0u;
     clog = 0ull;
     clog_len = 0u;
-    s = 0;
-    acc_mask = prop_mask = 0u;
-    stepped = pcur = 0u;
+    occ = 0u;
+    iso = 0u;
     bailed = false;
-    mode = M_PROP;
+    mode = M_RUN;
+    enter(0);
   }
 
   // broadcast o = (kind, x, z) by proposer q: bookkeeping of bcast() (oracle)
-  // and a pending entry whose N copies go out one per micro-step
-  __host__ __device__ void broadcast(uint32_t q, uint32_t kind, uint32_t x, uint32_t z, bool pred) {
+  // and a pending entry whose N copies go out one per iteration
+  __host__ __device__ __forceinline__ void broadcast(uint32_t q, uint32_t kind, uint32_t x, uint32_t z, bool pred) {
     rounds += (pred && kind == ASK) ? 1u : 0u;
     const bool ex = pred && kind == EXECUTE;
     execs += ex ? 1u : 0u;
     if (ex && dval == 0u) {                          // the decided value: first Execute (Client.hs:178)
-      dval = getp(r2_v, q);
+      dval = get(r2_v, q);
       dtick = x;
     }
-    const uint32_t slot = getp(bnext, q);
-    const uint32_t busy = (getp(refc, q) >> (4u * slot)) & 15u;
+    const uint32_t slot = get(bnext, q);
+    const uint32_t busy = (get(refc, q) >> (4u * slot)) & 15u;
     if (pred && busy != 0u) bailed = true;           // ring slot still referenced by a queued copy
     if (pred) {
       m.st16(S::BRING, q * BR + slot, x | (z << 12) | (kind << 14));
-      setp(bnext, q, (slot + 1u) & (BR - 1u));
       pq |= ((q << 3) | slot) << (5u * pq_len);
       pq_len += 1u;
     }
+    set(bnext, q, (slot + 1u) & (BR - 1u), pred);
   }
 
-  // the proposer q still has input this step (its Tick or a due response)
-  __host__ __device__ bool has_input(uint32_t q) const {
-    return ((tickp >> q) & 1u) != 0u || ctz32(prop_mask) < (q + 1u) * (uint32_t)N;
-  }
-
-  // move past proposers without input left: per (proposer, step) with input
-  // the canonical accounting charges 48 B (SEMANTICS §8)
-  __host__ __device__ void skip_idle() {
-#pragma unroll
-    for (int i = 0; i < PM; ++i) {
-      if (pcur < P && !has_input(pcur)) {
-        canon += ((stepped >> pcur) & 1u) ? 48u : 0u;
-        pcur += 1u;
-      }
-    }
-  }
-
-  // one micro-step; returns true when the instance ended (outputs in o)
-  __host__ __device__ bool step(const EvParams& kp, EvOut& o) {
-    bool snd = false;
-    uint32_t sdir = 0, sp = 0, sa = 0, sword = 0, sk = 0;
-
-    // ---------------- acceptor: one request (Server.hs:51-78) ----------------
-    if (mode == M_ACC) {
-      const uint32_t L = ctz32(acc_mask);
-      const uint32_t a = L / PM, p = L - a * PM;
-      const uint32_t rm = m.ld(S::REQM + L);
-      const uint32_t len = rm >> 28;
-      const uint32_t bslot = rm & 7u;
-      const uint32_t rm2 = ((rm & 0x0FFFFFFFu) >> 7) | ((len - 1u) << 28);
-      m.st(S::REQM + L, rm2);
-      const bool keep = len > 1u && ((rm2 >> 3) & 15u) == ((uint32_t)s & 15u);
-      acc_mask = keep ? acc_mask : (acc_mask & ~(1u << L));
-      in_flight -= 1u;
-      const uint32_t w16 = m.ld16(S::BRING, p * BR + bslot);
-      setp(refc, p, getp(refc, p) - (1u << (4u * bslot)));
-      const uint32_t kind = w16 >> 14, x = w16 & 0xFFFu, z = (w16 >> 12) & 3u;
-      uint32_t A = m.ld(S::ACCW + a);
-      const uint32_t win = m.ld(S::ACCC + a);
-      const bool iso = (win & 0xFFFFu) <= (uint32_t)s && (uint32_t)s < (win >> 16);
-      const bool dead = ((A >> 26) & 1u) != 0u;
-      const uint32_t rb = (kind == PROPOSE) ? 12u : 8u;
-      if (dead || iso) {
-        canon += rb;                                 // discarded at a dead / isolated acceptor
-      } else {
-        canon += 2u * rb + 32u;
-        const uint32_t t_max = A & 0xFFFu, t_store = (A >> 12) & 0xFFFu, val = (A >> 24) & 3u;
-        uint32_t log_len = A >> 27;
-        const bool is_ask = kind == ASK, is_prop = kind == PROPOSE, is_exec = kind == EXECUTE;
-        const bool grant = is_ask && !(t_max >= x);              // Server.hs:56
-        const bool accept = is_prop && x == t_max;               // :66 (equality, not >=)
-        const bool hit = is_exec && t_max == x;                  // :75
-        const bool panic = hit && val == 0u;                     // :76 (Q6)
-        const bool run = hit && val != 0u;                       // :77-78
-        const uint32_t rk = grant ? R1OK : accept ? R2S : (is_ask || is_prop) ? HAVE : 3u;
-        const uint32_t rx = grant ? x : (accept ? 0u : t_max);
-        const uint32_t ry = grant ? t_store : 0u;
-        const uint32_t rz = grant ? val : 0u;
-        const uint32_t nt_max = grant ? x : t_max;
-        const uint32_t nt_store = accept ? x : (run ? 0u : t_store);
-        const uint32_t nval = accept ? z : (run ? 0u : val);
-        lflags |= panic ? (uint32_t)PXB_F_PANIC : 0u;
-        if (run) {                                   // executed <>= [c]: log, digest, divergence
-          if (log_len >= 31u) bailed = true;
-          const uint32_t dg = m.ld(S::ACCD + a);
-          m.st(S::ACCD + a, fnv_u32(dg, (val << 24) | 1u));
-          if (log_len < clog_len) {
-            if (((uint32_t)(clog >> (2u * log_len)) & 3u) != val) lflags |= PXB_F_LOG_DIVERGENCE;
-          } else {
-            clog |= (unsigned long long)val << (2u * log_len);
-            clog_len += 1u;
-          }
-          log_len += 1u;
-        }
-        A = nt_max | (nt_store << 12) | (nval << 24) | ((dead || panic) ? (1u << 26) : 0u) | (log_len << 27);
-        m.st(S::ACCW + a, A);
-        if (rk != 3u) {                              // the reply, on link a -> p
-          snd = true;
-          sdir = 1u;
-          sp = p;
-          sa = a;
-          sword = rx | (ry << 12) | (rz << 24) | (rk << 30);
-        }
-      }
-      if (acc_mask == 0u) mode = M_PROP;
-    }
-
-    // ---------------- proposers: Tick, then responses in (a, seq) order -------
-    if (mode == M_PROP) {
-      skip_idle();
-      // the next copy of a pending broadcast (sendToAllServers, Client.hs:122-123)
-      if (!snd && pq_len != 0u) {
-        const uint32_t e = pq & 31u;
-        snd = true;
-        sdir = 0u;
-        sp = e >> 3;
-        sa = acur;
-        sword = e & 7u;
-        sk = getp(nsent, sp);                         // the broadcast's index = the link's seq
-        acur += 1u;
-        if (acur == (uint32_t)N) {
-          pq >>= 5;
-          pq_len -= 1u;
-          acur = 0u;
-          setp(nsent, sp, getp(nsent, sp) + 1u);
-        }
-      }
-      // one input of proposer pcur (room for the up to two broadcasts it may make)
-      if (pcur < P && pq_len + 2u <= PQ_CAP) {
-        const uint32_t q = pcur;
-        uint32_t T = getp(ticket, q), R = getp(rs, q), K = getp(acks, q);
-        uint32_t MT = getp(mr_t, q), MV = getp(mr_v, q), C2 = getp(r2_v, q), PD = getp(pending, q), CM = getp(cmd, q);
-        uint32_t k0o = NONE, x0o = 0, z0o = 0;
-        bool b1 = false;                              // the restart's AskForTicket (Client.hs:185)
-        stepped |= 1u << q;
-        if ((tickp >> q) & 1u) {                      // handleTick, Client.hs:196-207
-          tickp &= ~(1u << q);
-          if (R == IDLE) {
-            T += 1u;
-            CM = q + 1u;
-            K = 0u;
-            R = ROUND1;
-            MT = MV = 0u;
-            k0o = ASK;
-            x0o = T;
-          }
-        } else {                                      // handleServerResponse, Client.hs:125-189
-          const uint32_t Lr = ctz32(prop_mask);
-          const uint32_t rm = m.ld(S::RSPM + Lr);
-          const uint32_t len = (rm >> (4 * S::IB)) & 7u;
-          const uint32_t im = (1u << S::IB) - 1u;
-          const uint32_t k = rm & im;
-          const uint32_t pe = m.ld(S::POOLW + k);
-          const uint32_t pn = (len > 1u) ? m.ld(S::POOLW + ((rm >> S::IB) & im)) : 0u;
-          pfree |= (pool_mask_t)1 << k;
-          m.st(S::RSPM + Lr, (((rm & ((1u << (4 * S::IB)) - 1u)) >> S::IB)) | ((len - 1u) << (4 * S::IB)) |
-                                 (rm & (15u << (4 * S::IB + 3))));
-          const bool keep = len > 1u && ((pn >> 26) & 15u) == ((uint32_t)s & 15u);
-          prop_mask = keep ? prop_mask : (prop_mask & ~(1u << Lr));
-          in_flight -= 1u;
-          const uint32_t kind = pe >> 30, x = pe & 0xFFFu, y = (pe >> 12) & 0xFFFu, z = (pe >> 24) & 3u;
-          canon += 2u * (16u >> kind);                // Round1OK 16, HaveTicket 8, Round2Success 4
-          const uint32_t maj = (uint32_t)N >> 1;      // haveMajority: acks > floor(N/2), :191-194
-          if (kind == HAVE) {                         // :128-140
-            if (R != IDLE && x >= T) {
-              T = x + 1u;
-              K = 0u;
-              R = ROUND1;
-              MT = MV = 0u;
-              k0o = ASK;
-              x0o = T;
-            }
-          } else if (kind == R1OK) {                  // :142-170
-            if (R == ROUND1 && T == x) {
-              K += 1u;
-              uint32_t mt = MT, mv = MV;              // mr <> MostRecent mp (Common.hs:61-65)
-              if (mv == 0u) {
-                mt = y;
-                mv = z;
-              } else if (z != 0u && !(mt >= y)) {
-                mt = y;
-                mv = z;
-              }
-              if (K <= maj) {
-                MT = mt;
-                MV = mv;
-              } else {                                // Q5: pending whenever mr is Just
-                C2 = (mv == 0u) ? CM : mv;
-                PD = (mv != 0u) ? 1u : 0u;
-                K = 0u;
-                R = ROUND2;
-                MT = MV = 0u;
-                k0o = PROPOSE;
-                x0o = x;
-                z0o = C2;
-              }
-            }
-          } else {                                    // Round2Success, :172-189 (no ticket: Q2)
-            if (R == ROUND2) {
-              K += 1u;
-              if (K > maj) {
-                k0o = EXECUTE;
-                x0o = T;
-                if (PD) {
-                  T += 1u;
-                  K = 0u;
-                  R = ROUND1;
-                  MT = MV = 0u;
-                  b1 = true;
-                } else {
-                  CM = 0u;
-                  K = 0u;
-                  R = IDLE;
-                }
-              }
-            }
-          }
-        }
-        setp(ticket, q, T);
-        setp(rs, q, R);
-        setp(acks, q, K);
-        setp(mr_t, q, MT);
-        setp(mr_v, q, MV);
-        setp(r2_v, q, C2);
-        setp(pending, q, PD);
-        setp(cmd, q, CM);
-        broadcast(q, k0o, x0o, z0o, k0o != NONE);
-        broadcast(q, ASK, T, 0u, b1);
-        skip_idle();
-      }
-    }
-
-    // ---------------- the micro-step's one send (SEMANTICS §5) ----------------
+  // the next copy of the oldest pending broadcast, on link cp -> ca (Philox
+  // seq = the broadcast index, the link's seq: every broadcast tries every acceptor)
+  __host__ __device__ __forceinline__ void copy_send(const EvParams& kp, uint32_t s4) {
+    const bool snd = pq_len != 0u;
+    const uint32_t ce = pq & 31u;
+    const uint32_t cp = ce >> 3, cslot = ce & 7u, ca = acur;
+    const uint32_t ck = get(nsent, cp);
     if (snd) {
-      msgs += 1u;
-      uint32_t k;
-      const uint32_t Lq = sa * PM + sp;              // request-link / reply-seq index
-      if (sdir == 0u) {
-        k = sk;                                       // every broadcast tries every acceptor
-      } else {
-        k = m.ld16(S::RSEQ, Lq);
-        if (k == 0xFFFFu) bailed = true;
-        m.st16(S::RSEQ, Lq, k + 1u);
-      }
-      uint32_t d = 1u;
-      bool ok = true;
-      if (faulty) {
-        const uint4 w = philox(lo, hi, k, (1u << 24) | (sdir << 16) | (sp << 8) | sa, kp.k0, kp.k1);
-        ok = !(lossy && w.x <= loss_m1);
-        d = 1u + mulhi_n(w.y, dmax);
-      }
-      if (ok) {
-        const uint32_t s4 = (uint32_t)s & 15u;
-        uint32_t due_rel, wbit;
-        if (sdir == 0u) {                            // request copy on link p -> a
-          const uint32_t rm = m.ld(S::REQM + Lq);
-          const uint32_t len = rm >> 28;
-          if (len >= CPHYS) bailed = true;
-          const uint32_t rel = len ? (((rm >> (7u * (len - 1u) + 3u)) & 15u) - s4) & 15u : 0u;
-          due_rel = d > rel ? d : rel;
-          const uint32_t ent = sword | (((s4 + due_rel) & 15u) << 3);
-          m.st(S::REQM + Lq, (rm & 0x0FFFFFFFu) | (ent << (7u * len)) | ((len + 1u) << 28));
-          setp(refc, sp, getp(refc, sp) + (1u << (4u * sword)));
-          wbit = 1u << Lq;
-        } else {                                     // reply on link a -> p
-          const uint32_t Lr = sp * (uint32_t)N + sa;
-          const uint32_t rm = m.ld(S::RSPM + Lr);
-          const uint32_t len = (rm >> (4 * S::IB)) & 7u;
-          if (len >= CPHYS || pfree == 0) bailed = true;
-          const uint32_t rel = len ? (((rm >> (4 * S::IB + 3)) & 15u) - s4) & 15u : 0u;
-          due_rel = d > rel ? d : rel;
-          const uint32_t due4 = (s4 + due_rel) & 15u;
-          const uint32_t k2 = (POOL > 32) ? (uint32_t)__builtin_ctzll((unsigned long long)pfree | (1ull << 63))
-                                          : ctz32((uint32_t)pfree) & 31u;
-          pfree &= ~((pool_mask_t)1 << k2);
-          m.st(S::POOLW + k2, sword | (due4 << 26));
-          m.st(S::RSPM + Lr, (rm & ((1u << (S::IB * len)) - 1u)) | (k2 << (S::IB * len)) | ((len + 1u) << (4 * S::IB)) |
-                                 (due4 << (4 * S::IB + 3)));
-          wbit = 1u << (S::WW == 1 ? (S::PSH + Lr) : Lr);
-        }
-        const uint32_t slot = ((uint32_t)s + due_rel) & (uint32_t)(W - 1);
-        const uint32_t wi = S::WHEEL + slot * S::WW + ((S::WW == 2 && sdir == 1u) ? 1u : 0u);
-        m.st(wi, m.ld(wi) | wbit);
-        in_flight += 1u;
+      acur += 1u;
+      if (acur == (uint32_t)N) {
+        pq >>= 5;
+        pq_len -= 1u;
+        acur = 0u;
+        set(nsent, cp, ck + 1u, true);
       }
     }
+    uint32_t d = 1u;
+    bool ok = true;
+    if (faulty) {
+      const uint4 w = philox(lo, hi, ck, (1u << 24) | (cp << 8) | ca, kp.k0, kp.k1);
+      ok = !(lossy && w.x <= loss_m1);
+      d = 1u + mulhi_n(w.y, dmax);
+    }
+    msgs += snd ? 1u : 0u;
+    if (snd && ok) {
+      const uint32_t Lq = ca * (uint32_t)PM + cp;
+      const uint32_t rq = m.ld(S::REQ + Lq);
+      const uint32_t qlen = rq >> 28;
+      if (qlen >= CPHYS) bailed = true;
+      const uint32_t rel = qlen ? (((rq >> (7u * (qlen - 1u) + 3u)) & 15u) - s4) & 15u : 0u;
+      const uint32_t due_rel = d > rel ? d : rel;
+      const uint32_t ent = cslot | (((s4 + due_rel) & 15u) << 3);
+      m.st(S::REQ + Lq, (rq & 0x0FFFFFFFu) | (ent << (7u * qlen)) | ((qlen + 1u) << 28));
+      set(refc, cp, get(refc, cp) + (1u << (4u * cslot)), true);
+      const uint32_t slot = ((uint32_t)s + due_rel) & WM;
+      m.orw(S::WHEEL + slot * S::WW, 1u << Lq);
+      occ |= 1u << slot;
+      in_flight += 1u;
+    }
+  }
 
-    // ---------------- end of step: quiescence, step cap, next step ------------
-    if (mode == M_PROP && pcur >= P && pq_len == 0u) {
+  // one iteration; returns true when the instance ended (outputs in o)
+  __host__ __device__ __forceinline__ bool step(const EvParams& kp, EvOut& o) {
+    const uint32_t s4 = (uint32_t)s & 15u;
+
+    // ================= ACC: one due request (Server.hs:51-78) =================
+    const bool acc = acc_mask != 0u;
+    const uint32_t L = acc ? ctz32(acc_mask) : 0u;
+    const uint32_t a = L / (uint32_t)PM, p = L - a * (uint32_t)PM;
+    const uint32_t rm = m.ld(S::REQ + L);
+    const uint32_t kr = m.ld16(S::RSEQ, L);           // the reply's link sequence number
+    const uint32_t len = rm >> 28;
+    const uint32_t bslot = rm & 7u;
+    const uint32_t rm2 = ((rm & 0x0FFFFFFFu) >> 7) | ((len - 1u) << 28);
+    if (acc) m.st(S::REQ + L, rm2);
+    const bool keep = len > 1u && ((rm2 >> 3) & 15u) == s4;
+    acc_mask = (acc && !keep) ? (acc_mask & ~(1u << L)) : acc_mask;
+    in_flight -= acc ? 1u : 0u;
+    const uint32_t w16 = m.ld16(S::BRING, p * BR + bslot);
+    set(refc, p, get(refc, p) - (1u << (4u * bslot)), acc);
+    const uint32_t kind = w16 >> 14, x = w16 & 0xFFFu, z = (w16 >> 12) & 3u;
+    const uint32_t A = get(accw, a);
+    const bool dead = ((A >> 26) & 1u) != 0u;
+    const bool live = acc && !dead && !((iso >> a) & 1u);
+    const uint32_t rb = (kind == PROPOSE) ? 12u : 8u;
+    canon += acc ? (live ? 2u * rb + 32u : rb) : 0u;
+    const uint32_t t_max = A & 0xFFFu, t_store = (A >> 12) & 0xFFFu, val = (A >> 24) & 3u;
+    uint32_t log_len = A >> 27;
+    const bool is_ask = live && kind == ASK, is_prop = live && kind == PROPOSE, is_exec = live && kind == EXECUTE;
+    const bool grant = is_ask && !(t_max >= x);                // Server.hs:56
+    const bool accept = is_prop && x == t_max;                 // :66 (equality, not >=)
+    const bool hit = is_exec && t_max == x;                    // :75
+    const bool panic = hit && val == 0u;                       // :76 (Q6)
+    const bool run = hit && val != 0u;                         // :77-78
+    const uint32_t rk = grant ? R1OK : accept ? R2S : HAVE;
+    const uint32_t rx = grant ? x : (accept ? 0u : t_max);
+    const uint32_t ry = grant ? t_store : 0u;
+    const uint32_t rz = grant ? val : 0u;
+    const uint32_t nt_max = grant ? x : t_max;
+    const uint32_t nt_store = accept ? x : (run ? 0u : t_store);
+    const uint32_t nval = accept ? z : (run ? 0u : val);
+    lflags |= panic ? (uint32_t)PXB_F_PANIC : 0u;
+    if (run) {                                       // executed <>= [c]: log, digest, divergence
+      if (log_len >= 31u) bailed = true;
+      const uint32_t dg = m.ld(S::ACCD + a);
+      m.st(S::ACCD + a, fnv_u32(dg, (val << 24) | 1u));
+      if (log_len < clog_len) {
+        if (((uint32_t)(clog >> (2u * log_len)) & 3u) != val) lflags |= PXB_F_LOG_DIVERGENCE;
+      } else {
+        clog |= (unsigned long long)val << (2u * log_len);
+        clog_len += 1u;
+      }
+      log_len += 1u;
+    }
+    set(accw, a, nt_max | (nt_store << 12) | (nval << 24) | ((dead || panic) ? (1u << 26) : 0u) | (log_len << 27),
+        live);
+    const bool snd1 = live && !is_exec;              // the reply, on link a -> p
+
+    // ================= COPY: copies of the oldest pending broadcasts =================
+#pragma unroll
+    for (int c = 0; c < PXB_EV_CPRE; ++c) copy_send(kp, s4);
+
+    // ================= PROP: one input of one proposer =================
+    const bool pin = in_mask != 0u && pq_len + 2u <= PQ_CAP;
+    {
+      const uint32_t j = pin ? ctz32(in_mask) : 0u;
+      const uint32_t q = j / (uint32_t)(N + 1);
+      const uint32_t r = j - q * (uint32_t)(N + 1);
+      const bool tick = pin && r == 0u;
+      const bool resp = pin && r != 0u;
+      const uint32_t ra = r - 1u;
+      const uint32_t Lr = q * (uint32_t)N + (resp ? ra : 0u);
+      const uint32_t rmr = m.ld(S::RSP + Lr);
+      const uint32_t rlen = (rmr >> (4 * S::IB)) & 7u;
+      const uint32_t im = (1u << S::IB) - 1u;
+      const uint32_t k = rmr & im;
+      const uint32_t pe = m.ld(S::POOLW + k);
+      const uint32_t pn = m.ld(S::POOLW + ((rmr >> S::IB) & im));
+      if (resp) {
+        pfree |= (pool_mask_t)1 << k;
+        m.st(S::RSP + Lr, ((rmr & ((1u << (4 * S::IB)) - 1u)) >> S::IB) | ((rlen - 1u) << (4 * S::IB)) |
+                              (rmr & (15u << (4 * S::IB + 3))));
+      }
+      const bool rkeep = resp && rlen > 1u && ((pn >> 26) & 15u) == s4;
+      in_mask = (pin && !rkeep) ? (in_mask & ~(1u << j)) : in_mask;
+      in_flight -= resp ? 1u : 0u;
+      const uint32_t rkind = pe >> 30, px = pe & 0xFFFu, py = (pe >> 12) & 0xFFFu, pz = (pe >> 24) & 3u;
+      canon += resp ? 2u * (16u >> rkind) : 0u;         // Round1OK 16, HaveTicket 8, Round2Success 4
+
+      uint32_t T = get(ticket, q), R = get(rs, q), K = get(acks, q);
+      uint32_t MT = get(mr_t, q), MV = get(mr_v, q), C2 = get(r2_v, q), PD = get(pending, q), CM = get(cmd, q);
+      uint32_t k0o = NONE, x0o = 0, z0o = 0;
+      bool b1 = false;                                // the restart's AskForTicket (Client.hs:185)
+      const uint32_t maj = (uint32_t)N >> 1;          // haveMajority: acks > floor(N/2), :191-194
+      // handleTick, Client.hs:196-207
+      const bool t_go = tick && R == IDLE;
+      // HaveTicket, :128-140
+      const bool h_go = resp && rkind == HAVE && R != IDLE && px >= T;
+      // Round1OK, :142-170
+      const bool o_go = resp && rkind == R1OK && R == ROUND1 && T == px;
+      const uint32_t K1 = K + 1u;
+      const bool o_take = MV == 0u || (pz != 0u && !(MT >= py));   // mr <> MostRecent mp (Common.hs:61-65)
+      const uint32_t mt = o_take ? py : MT, mv = o_take ? pz : MV;
+      const bool o_maj = o_go && K1 > maj;
+      // Round2Success, :172-189 (no ticket: Q2)
+      const bool s_go = resp && rkind == R2S && R == ROUND2;
+      const bool s_maj = s_go && K1 > maj;
+      // the new state
+      const bool restart = t_go || h_go || (s_maj && PD);          // -> Round1 with a new ticket
+      const uint32_t Tn = t_go ? T + 1u : h_go ? px + 1u : (s_maj && PD) ? T + 1u : T;
+      k0o = (t_go || h_go) ? ASK : o_maj ? PROPOSE : s_maj ? EXECUTE : NONE;
+      x0o = (t_go || h_go) ? Tn : o_maj ? px : T;
+      const uint32_t C2n = o_maj ? ((mv == 0u) ? CM : mv) : C2;    // Q5: pending whenever mr is Just
+      z0o = C2n;
+      b1 = s_maj && PD != 0u;
+      set(ticket, q, Tn, pin);
+      set(rs, q, restart ? ROUND1 : o_maj ? ROUND2 : (s_maj ? IDLE : R), pin);
+      set(acks, q, (restart || o_maj || s_maj) ? 0u : ((o_go || s_go) ? K1 : K), pin);
+      set(mr_t, q, (restart || o_maj) ? 0u : (o_go ? mt : MT), pin);
+      set(mr_v, q, (restart || o_maj) ? 0u : (o_go ? mv : MV), pin);
+      set(r2_v, q, C2n, pin);
+      set(pending, q, o_maj ? ((mv != 0u) ? 1u : 0u) : PD, pin);
+      set(cmd, q, t_go ? q + 1u : (s_maj && !PD) ? 0u : CM, pin);
+      broadcast(q, k0o, x0o, z0o, k0o != NONE);
+      broadcast(q, ASK, Tn, 0u, b1);
+    }
+#pragma unroll
+    for (int c = 0; c < PXB_EV_CPOST; ++c) copy_send(kp, s4);
+
+    // ================= the iteration's sends (SEMANTICS §5) =================
+    // reply on a -> p (Philox seq = the link's reply count)
+    uint32_t d1 = 1u;
+    bool ok1 = true;
+    if (faulty) {
+      const uint4 w1 = philox(lo, hi, kr, (1u << 24) | (1u << 16) | (p << 8) | a, kp.k0, kp.k1);
+      ok1 = !(lossy && w1.x <= loss_m1);
+      d1 = 1u + mulhi_n(w1.y, dmax);
+    }
+    if (snd1) {
+      msgs += 1u;
+      if (kr == 0xFFFFu) bailed = true;
+      m.st16(S::RSEQ, L, kr + 1u);
+    }
+    if (snd1 && ok1) {
+      const uint32_t Lr = p * (uint32_t)N + a;
+      const uint32_t rmr = m.ld(S::RSP + Lr);
+      const uint32_t rlen = (rmr >> (4 * S::IB)) & 7u;
+      if (rlen >= CPHYS || pfree == 0) bailed = true;
+      const uint32_t rel = rlen ? (((rmr >> (4 * S::IB + 3)) & 15u) - s4) & 15u : 0u;
+      const uint32_t due_rel = d1 > rel ? d1 : rel;
+      const uint32_t due4 = (s4 + due_rel) & 15u;
+      const uint32_t k2 = (POOL > 32) ? (uint32_t)__builtin_ctzll((unsigned long long)pfree | (1ull << 63))
+                                      : ctz32((uint32_t)pfree) & 31u;
+      pfree &= ~((pool_mask_t)1 << k2);
+      m.st(S::POOLW + k2, rx | (ry << 12) | (rz << 24) | (due4 << 26) | (rk << 30));
+      m.st(S::RSP + Lr, (rmr & ((1u << (S::IB * rlen)) - 1u)) | (k2 << (S::IB * rlen)) |
+                            ((rlen + 1u) << (4 * S::IB)) | (due4 << (4 * S::IB + 3)));
+      const uint32_t slot = ((uint32_t)s + due_rel) & WM;
+      const uint32_t wi = S::WHEEL + slot * S::WW + (S::WW == 2 ? 1u : 0u);
+      m.orw(wi, 1u << (S::ISH + p * (N + 1) + 1u + a));
+      occ |= 1u << slot;
+      in_flight += 1u;
+    }
+    // ================= END of step: quiescence, step cap, next step =================
+    if (acc_mask == 0u && in_mask == 0u && pq_len == 0u) {
       const bool quiet = in_flight == 0u && s >= last_tick;
-      if (quiet || s + 1 >= (int32_t)kp.step_cap) {
-        finish(!quiet, o);
+      if (quiet) {
+        finish(false, o);
         return true;
       }
-      s += 1;
-      const uint32_t slot = (uint32_t)s & (uint32_t)(W - 1);
-      if (S::WW == 1) {
-        const uint32_t wv = m.ld(S::WHEEL + slot);
-        m.st(S::WHEEL + slot, 0u);
-        acc_mask = wv & 0xFFFFu;
-        prop_mask = wv >> 16;
-      } else {
-        acc_mask = m.ld(S::WHEEL + 2 * slot);
-        prop_mask = m.ld(S::WHEEL + 2 * slot + 1);
-        m.st(S::WHEEL + 2 * slot, 0u);
-        m.st(S::WHEEL + 2 * slot + 1, 0u);
-      }
-      tickp = 0u;
+      // the next step with a due message or a Tick
+      const uint32_t s1 = (uint32_t)s + 1u;
+      const uint32_t rot = ((occ >> (s1 & WM)) | (occ << ((W - (s1 & WM)) & WM))) & ((1u << W) - 1u);
+      uint32_t nx = occ ? s1 + ctz32(rot) : 0xFFFFu;
 #pragma unroll
-      for (int p = 0; p < PM; ++p) tickp |= ((uint32_t)p < P && skew[p] == (uint32_t)s) ? (1u << p) : 0u;
-      pcur = 0u;
-      stepped = 0u;
-      mode = acc_mask ? M_ACC : M_PROP;
+      for (int q = 0; q < PM; ++q)
+        nx = ((uint32_t)q < P && skew[q] > (uint32_t)s && skew[q] < nx) ? skew[q] : nx;
+      if (nx >= kp.step_cap) {
+        s = (int32_t)kp.step_cap - 1;
+        finish(true, o);
+        return true;
+      }
+      enter((int32_t)nx);
     }
     return false;
   }
 
   // ---- outputs of an ended instance (SEMANTICS §7) ----
-  __host__ __device__ void finish(bool capped, EvOut& o) {
+  __host__ __device__ __forceinline__ void finish(bool capped, EvOut& o) {
     const uint32_t steps = (uint32_t)s + 1u;
     uint32_t f = lflags | (capped ? (uint32_t)PXB_F_STEP_CAP : 0u) | (dval ? 0u : (uint32_t)PXB_F_UNDECIDED);
 #pragma unroll
@@ -581,11 +585,9 @@ struct EvLane {
   }
 
   // final per-acceptor outputs (digest, record) of an ended instance
-  __host__ __device__ uint32_t digest_of(int a) const {
-    return fnv_u32(m.ld(S::ACCD + a), m.ld(S::ACCW + a) >> 27);
-  }
+  __host__ __device__ uint32_t digest_of(int a) const { return fnv_u32(m.ld(S::ACCD + a), accw[a] >> 27); }
   __host__ __device__ void record_of(int a, uint32_t r[4]) const {
-    const uint32_t A = m.ld(S::ACCW + a);
+    const uint32_t A = accw[a];
     const uint32_t val = (A >> 24) & 3u;
     r[0] = A & 0xFFFu;
     r[1] = (A >> 12) & 0xFFFu;

@@ -25,6 +25,8 @@ struct LdsMem {
   __host__ __device__ void st16(uint32_t base, uint32_t i, uint32_t v) const {
     reinterpret_cast<uint16_t*>(w)[((base + (i >> 1)) * 64u + lane) * 2u + (i & 1u)] = (uint16_t)v;
   }
+  // OR into a word (ds_or_b32: no read-back on the critical path)
+  __device__ void orw(uint32_t i, uint32_t v) const { atomicOr(&w[i * 64u + lane], v); }
 };
 
 constexpr uint32_t EV_QCHUNK = 64;            // instances per work-queue grab (one per lane)
