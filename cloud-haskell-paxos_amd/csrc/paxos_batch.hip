@@ -30,11 +30,12 @@ PXB_FOR_MODES(PXB_EXTERN, 1)
 PXB_FOR_MODES(PXB_EXTERN, 2)
 PXB_FOR_MODES(PXB_EXTERN, 3)
 // per-lane kernels (paxos_ev.hip): P x N x {8, 16}-step wheels
-#define PXB_EV_EXTERN(PM, N, W) extern template __global__ void ev::paxos_ev_kernel<PM, N, W>(ev::EvKParams);
-#define PXB_EV_FOR(M, PM, W) M(PM, 2, W) M(PM, 3, W) M(PM, 4, W) M(PM, 5, W) M(PM, 6, W) M(PM, 7, W) M(PM, 8, W) M(PM, 9, W)
-PXB_EV_FOR(PXB_EV_EXTERN, 1, 8) PXB_EV_FOR(PXB_EV_EXTERN, 1, 16)
-PXB_EV_FOR(PXB_EV_EXTERN, 2, 8) PXB_EV_FOR(PXB_EV_EXTERN, 2, 16)
-PXB_EV_FOR(PXB_EV_EXTERN, 3, 8) PXB_EV_FOR(PXB_EV_EXTERN, 3, 16)
+#define PXB_EV_EXTERN(PM, N, W, C) extern template __global__ void ev::paxos_ev_kernel<PM, N, W, C>(ev::EvKParams);
+#define PXB_EV_FOR(M, PM, W, C) M(PM, 2, W, C) M(PM, 3, W, C) M(PM, 4, W, C) M(PM, 5, W, C) M(PM, 6, W, C) \
+  M(PM, 7, W, C) M(PM, 8, W, C) M(PM, 9, W, C)
+PXB_EV_FOR(PXB_EV_EXTERN, 1, 8, false) PXB_EV_FOR(PXB_EV_EXTERN, 1, 16, false) PXB_EV_FOR(PXB_EV_EXTERN, 1, 8, true)
+PXB_EV_FOR(PXB_EV_EXTERN, 2, 8, false) PXB_EV_FOR(PXB_EV_EXTERN, 2, 16, false) PXB_EV_FOR(PXB_EV_EXTERN, 2, 8, true)
+PXB_EV_FOR(PXB_EV_EXTERN, 3, 8, false) PXB_EV_FOR(PXB_EV_EXTERN, 3, 16, false) PXB_EV_FOR(PXB_EV_EXTERN, 3, 8, true)
 
 // ---- single-handler hook kernels ------------------------------------------
 __global__ void acceptor_hook_kernel(pxb_acceptor_rec* st, const pxb_msg* in, pxb_msg* out, uint32_t count) {
@@ -102,29 +103,33 @@ __global__ __launch_bounds__(TCOPIES) void finalize_kernel(unsigned long long* p
 typedef void (*kernel_ptr)(KParams);
 typedef void (*ev_kernel_ptr)(ev::EvKParams);
 
-template <int PM, int W>
+template <int PM, int W, bool C>
 static ev_kernel_ptr ev_pick_n(uint32_t n) {
   switch (n) {
-    case 2: return ev::paxos_ev_kernel<PM, 2, W>;
-    case 3: return ev::paxos_ev_kernel<PM, 3, W>;
-    case 4: return ev::paxos_ev_kernel<PM, 4, W>;
-    case 5: return ev::paxos_ev_kernel<PM, 5, W>;
-    case 6: return ev::paxos_ev_kernel<PM, 6, W>;
-    case 7: return ev::paxos_ev_kernel<PM, 7, W>;
-    case 8: return ev::paxos_ev_kernel<PM, 8, W>;
-    case 9: return ev::paxos_ev_kernel<PM, 9, W>;
+    case 2: return ev::paxos_ev_kernel<PM, 2, W, C>;
+    case 3: return ev::paxos_ev_kernel<PM, 3, W, C>;
+    case 4: return ev::paxos_ev_kernel<PM, 4, W, C>;
+    case 5: return ev::paxos_ev_kernel<PM, 5, W, C>;
+    case 6: return ev::paxos_ev_kernel<PM, 6, W, C>;
+    case 7: return ev::paxos_ev_kernel<PM, 7, W, C>;
+    case 8: return ev::paxos_ev_kernel<PM, 8, W, C>;
+    case 9: return ev::paxos_ev_kernel<PM, 9, W, C>;
   }
   return nullptr;
 }
 
-static ev_kernel_ptr ev_pick(uint32_t pm, uint32_t n, int w) {
-  switch (pm * 100 + (uint32_t)w) {
-    case 108: return ev_pick_n<1, 8>(n);
-    case 116: return ev_pick_n<1, 16>(n);
-    case 208: return ev_pick_n<2, 8>(n);
-    case 216: return ev_pick_n<2, 16>(n);
-    case 308: return ev_pick_n<3, 8>(n);
-    case 316: return ev_pick_n<3, 16>(n);
+// layout index: 0 = 8-step wheel, 1 = 16-step wheel, 2 = compact links (8-step wheel)
+static ev_kernel_ptr ev_pick(uint32_t pm, uint32_t n, int layout) {
+  switch (pm * 10 + (uint32_t)layout) {
+    case 10: return ev_pick_n<1, 8, false>(n);
+    case 11: return ev_pick_n<1, 16, false>(n);
+    case 12: return ev_pick_n<1, 8, true>(n);
+    case 20: return ev_pick_n<2, 8, false>(n);
+    case 21: return ev_pick_n<2, 16, false>(n);
+    case 22: return ev_pick_n<2, 8, true>(n);
+    case 30: return ev_pick_n<3, 8, false>(n);
+    case 31: return ev_pick_n<3, 16, false>(n);
+    case 32: return ev_pick_n<3, 8, true>(n);
   }
   return nullptr;
 }
@@ -189,7 +194,7 @@ static uint32_t g_qseq[64];
 // blocks per CU by [wheel][pm][n][device]
 constexpr uint64_t EV_CHUNK = 1ull << 21;
 static uint32_t* g_bail[64][QSLOTS];
-static int g_eocc[2][4][10][64];
+static int g_eocc[3][4][10][64];
 
 static int hip_fail(hipError_t e) {
   g_last_hip = (int)e;
@@ -282,8 +287,8 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
   const bool use_ev = !ff && !logm && ev::eligible(cfg) && !(no_ev && atoi(no_ev) > 0);
   kernel_fn fn = pick(cfg->n_proposers, cfg->n_acceptors, logm, ff);
   if (!fn) return PXB_E_INVAL;
-  const int wheel = ev::wheel_for(cfg->delay_max);
-  const ev_kernel_ptr efn = use_ev ? ev_pick(cfg->n_proposers, cfg->n_acceptors, wheel) : nullptr;
+  const int layout = ev::layout_for(cfg);
+  const ev_kernel_ptr efn = use_ev ? ev_pick(cfg->n_proposers, cfg->n_acceptors, layout) : nullptr;
   if (use_ev && !efn) return PXB_E_INVAL;
   const hipStream_t st = (hipStream_t)stream;
   int occ, cus, eocc = 0;
@@ -307,7 +312,7 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
     occ = std::min(o, std::max(1, target / fn.wpb));   // blocks per CU
     cus = g_cus[dev];
     if (use_ev) {
-      int& eo = g_eocc[(wheel == 8) ? 0 : 1][cfg->n_proposers][cfg->n_acceptors][dev];
+      int& eo = g_eocc[layout][cfg->n_proposers][cfg->n_acceptors][dev];
       if (!eo) {
         int nb = 0;
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)efn, 64, 0));

@@ -26,12 +26,24 @@ constexpr uint32_t IDLE = 0, ROUND1 = 1, ROUND2 = 2;
 // Each round needs the full 64-bit products of two 32-bit words: written as
 // 64-bit multiplies they compile to one v_mad_u64_u32 each instead of a
 // v_mul_lo_u32 + v_mul_hi_u32 pair.
+// three-input xor as one gfx950 v_bitop3_b32 (truth table 0x96); LLVM emits
+// two v_xor_b32 for it
+__host__ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t r;
+  __asm__("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+  return r;
+#else
+  return a ^ b ^ c;
+#endif
+}
+
 __host__ __device__ __forceinline__ uint4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
                                         uint32_t k0, uint32_t k1) {
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
     const uint64_t p0 = (uint64_t)c0 * 0xD2511F53u, p1 = (uint64_t)c2 * 0xCD9E8D57u;
-    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    const uint32_t n0 = xor3((uint32_t)(p1 >> 32), c1, k0), n2 = xor3((uint32_t)(p0 >> 32), c3, k1);
     c1 = (uint32_t)p1;
     c3 = (uint32_t)p0;
     c0 = n0;

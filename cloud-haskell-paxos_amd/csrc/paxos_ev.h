@@ -59,7 +59,6 @@
 namespace pxb {
 namespace ev {
 
-constexpr uint32_t CPHYS = 4;     // physical FIFO slots per link
 constexpr uint32_t BR = 8;        // broadcast ring slots per proposer
 constexpr uint32_t PQ_CAP = 4;    // pending broadcasts per lane
 constexpr uint32_t MAX_STEP_CAP = 4095;   // 12-bit tickets (tickets <= step_cap, SEMANTICS §6)
@@ -68,31 +67,42 @@ static_assert(MAX_STEP_CAP < PXB_TICKET_LIMIT, "EV tickets never reach the overf
 // lane modes
 constexpr uint32_t M_IDLE = 0, M_RUN = 1;
 
-template <int PM_, int N_, int POOL_, int W_>
+template <int PM_, int N_, int POOL_, int W_, bool CMP_>
 struct Shape {
   static constexpr int PM = PM_, N = N_, POOL = POOL_, W = W_;
+  static constexpr bool CMP = CMP_;                  // compact links (see Layouts)
   static constexpr int NLQ = PM * N;                 // request (and response) links
   static constexpr int NIN = PM * (N + 1);           // proposer-input bits (Tick + N links each)
   static constexpr int WW = (NLQ + NIN <= 32) ? 1 : 2;   // wheel words per slot
   static constexpr int ISH = (WW == 1) ? NLQ : 0;    // input-bit offset in its wheel word
   static constexpr int IB = POOL <= 32 ? 5 : 6;      // pool index bits
+  // request FIFO: QC entries of 7 bits, length at QL (QLB bits); compact: the
+  // reply seq of the same (a, p) pair in the word's top KB bits
+  static constexpr int QC = CMP ? 3 : 4, QL = 7 * QC, QLB = CMP ? 2 : 3;
+  static constexpr int KSH = QL + QLB, KB = 32 - KSH;
+  // response FIFO: RC pool indices of IB bits, length at RL (RLB bits), tail due at RD
+  static constexpr int RC = 4, RL = IB * RC, RLB = 3, RD = RL + RLB;
   // LDS word offsets
-  static constexpr int REQ = 0;                      // NLQ: request links, index a*PM + p
-  static constexpr int RSP = REQ + NLQ;              // NLQ: response links, index p*N + a
-  static constexpr int RSEQ = RSP + NLQ;             // NLQ halfwords: reply seq, index a*PM + p
-  static constexpr int POOLW = RSEQ + (NLQ + 1) / 2; // POOL response words
+  static constexpr int REQ = 0;                      // NLQ: request links, index a*PM + p (CMP: + reply seq)
+  static constexpr int RSEQ = REQ + NLQ;             // !CMP: NLQ halfwords of reply seq, index a*PM + p
+  static constexpr int RSP = RSEQ + (CMP ? 0 : (NLQ + 1) / 2);   // NLQ response links, index p*N + a
+  static constexpr int POOLW = RSP + NLQ;            // POOL response words
   static constexpr int BRING = POOLW + POOL;         // PM*BR halfwords: broadcast payloads
-  static constexpr int ACCD = BRING + PM * BR / 2;   // N digests
-  static constexpr int WHEEL = ACCD + N;             // W * WW due masks
-  static constexpr int WORDS = WHEEL + W * WW;
+  static constexpr int WHEEL = BRING + PM * BR / 2;  // W * WW due masks
+  static constexpr int DUMMY = WHEEL + W * WW;       // 1: target of the stores of inactive lanes
+  static constexpr int WORDS = DUMMY + 1;
   static_assert(W == 8 || W == 16, "wheel of 8 or 16 steps");
   static_assert(NIN <= 32 && NLQ <= 32, "masks are 32-bit");
-  static_assert(4 * IB + 7 <= 32, "response-link word");
+  static_assert(RD + 4 <= 32, "response-link word");
+  static_assert(QL + QLB <= 31, "request-link word");
 };
 
 // Layouts (docs/SEMANTICS.md §2 encodings; tickets < 2^12):
-//   request-link word   entry i (7 bits at 7i): broadcast slot [2:0] | due&15 [6:3];  len [30:28]
-//   response-link word  pool index i (IB bits at IB*i); len [4IB+2:4IB]; last due&15 [4IB+6:4IB+3]
+//   request-link word   entry i (7 bits at 7i): broadcast slot [2:0] | due&15 [6:3]; len at QL
+//                       (compact: 3 entries, len [22:21], and the reply seq of the same
+//                       (a, p) pair in [31:23], one word for both; else 4 entries, len
+//                       [30:28], reply seq in its own halfword)
+//   response-link word  pool index i (IB bits at IB*i); len [4IB+2:4IB]; last due&15 above it
 //   response word       x [11:0] | y [23:12] | z [25:24] | kind [31:30]
 //   broadcast payload   x [11:0] | z [13:12] | kind [15:14]
 //   acceptor word       t_max [11:0] | t_store [23:12] | val [25:24] | dead [26] | log_len [31:27]
@@ -112,6 +122,7 @@ struct EvParams {
   uint32_t crash_len_max, crash_start_max, skew_max, step_cap;
 };
 constexpr uint32_t EV_CFG_RANDOMIZE = 1u << 0, EV_CFG_LOSSY = 1u << 1, EV_CFG_CRASHY = 1u << 2;
+constexpr uint32_t EV_CFG_DRAWS = 1u << 3;    // some instance may draw message loss / delay
 
 __host__ __device__ inline uint64_t ev_threshold(uint32_t ppm) {
   return ((((uint64_t)ppm) << 32) + 999999ull) / 1000000ull;
@@ -134,12 +145,14 @@ struct EvOut {
 #define PXB_EV_CPOST 1
 #endif
 
-template <int PM, int N, int POOL, int W, class Mem>
+template <int PM, int N, int POOL, int W, bool CMP, class Mem>
 struct EvLane {
-  using S = Shape<PM, N, POOL, W>;
+  using S = Shape<PM, N, POOL, W, CMP>;
   using pool_mask_t = typename std::conditional<(POOL > 32), unsigned long long, uint32_t>::type;
   static constexpr uint32_t NLQ = S::NLQ;
   static constexpr uint32_t WM = (uint32_t)W - 1u;
+  static constexpr uint32_t QLM = (1u << S::QLB) - 1u, RLM = (1u << S::RLB) - 1u;
+  static constexpr uint32_t IM = (1u << S::IB) - 1u;
 
   Mem m;
   // ---- instance ----
@@ -159,8 +172,8 @@ struct EvLane {
   uint32_t nsent[PM];                 // broadcasts of p whose copies have started (request-link seq)
   uint32_t bnext[PM];                 // next broadcast-ring slot
   uint32_t refc[PM];                  // ring-slot reference counts (4-bit nibbles)
-  // acceptor states (Server.hs:24-31) and isolation windows
-  uint32_t accw[N], win[N];
+  // acceptor states (Server.hs:24-31), isolation windows, log digests
+  uint32_t accw[N], win[N], accd[N];
   uint32_t pq, pq_len, acur;          // pending broadcasts (p << 3 | slot, 5 bits each), next acceptor
   pool_mask_t pfree;                  // free response-pool words
   uint32_t in_flight;
@@ -184,6 +197,15 @@ struct EvLane {
 #endif
     return x;
   }
+  // the Philox key re-read inside the loop: its ten round keys are then two
+  // SALU adds per round, instead of twenty loop-invariant SGPRs that push
+  // the lane predicates into VGPR spill slots
+  __host__ __device__ static __forceinline__ uint32_t skey(uint32_t k) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __asm__ volatile("" : "+s"(k));
+#endif
+    return k;
+  }
   template <int K>
   __host__ __device__ static __forceinline__ uint32_t get(const uint32_t (&v)[K], uint32_t q) {
     uint32_t r = opaque(v[0]);
@@ -196,6 +218,9 @@ struct EvLane {
 #pragma unroll
     for (int i = 0; i < K; ++i) v[i] = (pred && q == (uint32_t)i) ? x : v[i];
   }
+
+  __host__ __device__ __forceinline__ uint32_t rsp_ld(uint32_t Lr) const { return m.ld(S::RSP + Lr); }
+  __host__ __device__ __forceinline__ void rsp_st(uint32_t Lr, uint32_t v) const { m.st(S::RSP + Lr, v); }
 
   __host__ __device__ __forceinline__ uint32_t iso_at(int32_t t) const {
     uint32_t r = 0u;
@@ -294,16 +319,11 @@ struct EvLane {
       anyiso = anyiso || c1 > c0;
       win[a] = c0 | (c1 << 16);
       accw[a] = 0u;
-      m.st(S::ACCD + a, 0x811C9DC5u);
+      accd[a] = 0x811C9DC5u;
     }
     crashy = anyiso;                                 // no window at all: skip the isolation test
 #pragma unroll
-    for (int L = 0; L < (int)NLQ; ++L) {
-      m.st(S::REQ + L, 0u);
-      m.st(S::RSP + L, 0u);
-    }
-#pragma unroll
-    for (int i = 0; i < ((int)NLQ + 1) / 2; ++i) m.st(S::RSEQ + i, 0u);
+    for (int i = S::REQ; i < S::POOLW; ++i) m.st(i, 0u);     // request links, reply seqs, response links
 #pragma unroll
     for (int i = 0; i < W * S::WW; ++i) m.st(S::WHEEL + i, 0u);
     pq = pq_len = acur = 0u;
@@ -331,19 +351,19 @@ struct EvLane {
     }
     const uint32_t slot = get(bnext, q);
     const uint32_t busy = (get(refc, q) >> (4u * slot)) & 15u;
-    if (pred && busy != 0u) bailed = true;           // ring slot still referenced by a queued copy
-    if (pred) {
-      m.st16(S::BRING, q * BR + slot, x | (z << 12) | (kind << 14));
-      pq |= ((q << 3) | slot) << (5u * pq_len);
-      pq_len += 1u;
-    }
+    bailed = bailed || (pred && busy != 0u);         // ring slot still referenced by a queued copy
+    m.st16(pred ? S::BRING : S::DUMMY, pred ? q * BR + slot : 0u, x | (z << 12) | (kind << 14));
+    pq |= pred ? ((q << 3) | slot) << (5u * pq_len) : 0u;
+    pq_len += pred ? 1u : 0u;
     set(bnext, q, (slot + 1u) & (BR - 1u), pred);
   }
 
   // the next copy of the oldest pending broadcast, on link cp -> ca (Philox
   // seq = the broadcast index, the link's seq: every broadcast tries every acceptor)
-  __host__ __device__ __forceinline__ void copy_send(const EvParams& kp, uint32_t s4) {
-    const bool snd = pq_len != 0u;
+  __host__ __device__ __forceinline__ bool copy_ready() const { return pq_len != 0u; }
+  __host__ __device__ __forceinline__ void copy_send(const EvParams& kp, bool act) {
+    const uint32_t s4 = (uint32_t)s & 15u;
+    const bool snd = act && pq_len != 0u;
     const uint32_t ce = pq & 31u;
     const uint32_t cp = ce >> 3, cslot = ce & 7u, ca = acur;
     const uint32_t ck = get(nsent, cp);
@@ -358,44 +378,53 @@ struct EvLane {
     }
     uint32_t d = 1u;
     bool ok = true;
-    if (faulty) {
-      const uint4 w = philox(lo, hi, ck, (1u << 24) | (cp << 8) | ca, kp.k0, kp.k1);
+    if (kp.cfg & EV_CFG_DRAWS) {                      // wave-uniform
+      const uint4 w = philox(lo, hi, ck, (1u << 24) | (cp << 8) | ca, skey(kp.k0), skey(kp.k1));
       ok = !(lossy && w.x <= loss_m1);
-      d = 1u + mulhi_n(w.y, dmax);
+      d = faulty ? 1u + mulhi_n(w.y, dmax) : 1u;
     }
     msgs += snd ? 1u : 0u;
-    if (snd && ok) {
-      const uint32_t Lq = ca * (uint32_t)PM + cp;
-      const uint32_t rq = m.ld(S::REQ + Lq);
-      const uint32_t qlen = rq >> 28;
-      if (qlen >= CPHYS) bailed = true;
-      const uint32_t rel = qlen ? (((rq >> (7u * (qlen - 1u) + 3u)) & 15u) - s4) & 15u : 0u;
-      const uint32_t due_rel = d > rel ? d : rel;
-      const uint32_t ent = cslot | (((s4 + due_rel) & 15u) << 3);
-      m.st(S::REQ + Lq, (rq & 0x0FFFFFFFu) | (ent << (7u * qlen)) | ((qlen + 1u) << 28));
-      set(refc, cp, get(refc, cp) + (1u << (4u * cslot)), true);
-      const uint32_t slot = ((uint32_t)s + due_rel) & WM;
-      m.orw(S::WHEEL + slot * S::WW, 1u << Lq);
-      occ |= 1u << slot;
-      in_flight += 1u;
-    }
+    // enqueue (predicated: inactive lanes store to the dummy word)
+    const bool go = snd && ok;
+    const uint32_t Lq = ca * (uint32_t)PM + cp;
+    const uint32_t wq = m.ld(S::REQ + Lq);
+    const uint32_t qlen = (wq >> S::QL) & QLM;
+    bailed = bailed || (go && qlen >= (uint32_t)S::QC);
+    const uint32_t rel = qlen ? (((wq >> (7u * (qlen - 1u) + 3u)) & 15u) - s4) & 15u : 0u;
+    const uint32_t due_rel = d > rel ? d : rel;
+    const uint32_t ent = cslot | (((s4 + due_rel) & 15u) << 3);
+    m.st(go ? S::REQ + Lq : S::DUMMY, (wq & ~(QLM << S::QL)) | (ent << (7u * qlen)) | ((qlen + 1u) << S::QL));
+    set(refc, cp, get(refc, cp) + (1u << (4u * cslot)), go);
+    const uint32_t slot = ((uint32_t)s + due_rel) & WM;
+    m.orw(go ? S::WHEEL + slot * S::WW : S::DUMMY, 1u << Lq);
+    occ |= go ? (1u << slot) : 0u;
+    in_flight += go ? 1u : 0u;
   }
 
-  // one iteration; returns true when the instance ended (outputs in o)
+  // one iteration of all four parts; returns true when the instance ended (outputs in o)
   __host__ __device__ __forceinline__ bool step(const EvParams& kp, EvOut& o) {
-    const uint32_t s4 = (uint32_t)s & 15u;
+    acc_op(kp, true);
+#pragma unroll
+    for (int c = 0; c < PXB_EV_CPRE; ++c) copy_send(kp, true);
+    prop_op(kp, true);
+#pragma unroll
+    for (int c = 0; c < PXB_EV_CPOST; ++c) copy_send(kp, true);
+    return end_op(kp, o, true);
+  }
 
-    // ================= ACC: one due request (Server.hs:51-78) =================
-    const bool acc = acc_mask != 0u;
+  // ================= ACC: one due request (Server.hs:51-78) and its reply =================
+  __host__ __device__ __forceinline__ bool acc_ready() const { return acc_mask != 0u; }
+  __host__ __device__ __forceinline__ void acc_op(const EvParams& kp, bool act) {
+    const uint32_t s4 = (uint32_t)s & 15u;
+    const bool acc = act && acc_mask != 0u;
     const uint32_t L = acc ? ctz32(acc_mask) : 0u;
     const uint32_t a = L / (uint32_t)PM, p = L - a * (uint32_t)PM;
-    const uint32_t rm = m.ld(S::REQ + L);
-    const uint32_t kr = m.ld16(S::RSEQ, L);           // the reply's link sequence number
-    const uint32_t len = rm >> 28;
-    const uint32_t bslot = rm & 7u;
-    const uint32_t rm2 = ((rm & 0x0FFFFFFFu) >> 7) | ((len - 1u) << 28);
-    if (acc) m.st(S::REQ + L, rm2);
-    const bool keep = len > 1u && ((rm2 >> 3) & 15u) == s4;
+    const uint32_t wq = m.ld(S::REQ + L);
+    const uint32_t kr = S::CMP ? (wq >> S::KSH) : m.ld16(S::RSEQ, L);   // the reply's link sequence number
+    const uint32_t len = (wq >> S::QL) & QLM;
+    const uint32_t bslot = wq & 7u;
+    const uint32_t rq2 = ((wq & ((1u << S::QL) - 1u)) >> 7) | ((len - 1u) << S::QL);
+    const bool keep = len > 1u && ((rq2 >> 3) & 15u) == s4;
     acc_mask = (acc && !keep) ? (acc_mask & ~(1u << L)) : acc_mask;
     in_flight -= acc ? 1u : 0u;
     const uint32_t w16 = m.ld16(S::BRING, p * BR + bslot);
@@ -424,8 +453,7 @@ struct EvLane {
     lflags |= panic ? (uint32_t)PXB_F_PANIC : 0u;
     if (run) {                                       // executed <>= [c]: log, digest, divergence
       if (log_len >= 31u) bailed = true;
-      const uint32_t dg = m.ld(S::ACCD + a);
-      m.st(S::ACCD + a, fnv_u32(dg, (val << 24) | 1u));
+      set(accd, a, fnv_u32(get(accd, a), (val << 24) | 1u), true);
       if (log_len < clog_len) {
         if (((uint32_t)(clog >> (2u * log_len)) & 3u) != val) lflags |= PXB_F_LOG_DIVERGENCE;
       } else {
@@ -437,13 +465,51 @@ struct EvLane {
     set(accw, a, nt_max | (nt_store << 12) | (nval << 24) | ((dead || panic) ? (1u << 26) : 0u) | (log_len << 27),
         live);
     const bool snd1 = live && !is_exec;              // the reply, on link a -> p
+    m.st(acc ? S::REQ + L : S::DUMMY, rq2 | (S::CMP ? ((kr + (snd1 ? 1u : 0u)) << S::KSH) : 0u));
 
-    // ================= COPY: copies of the oldest pending broadcasts =================
-#pragma unroll
-    for (int c = 0; c < PXB_EV_CPRE; ++c) copy_send(kp, s4);
+    // ================= the reply, on a -> p (SEMANTICS §5) =================
+    // Philox seq = the link's reply count.  Sent before the proposer part so its
+    // state dies early; the proposer part only pops due-now heads, so the order
+    // of the two on one link does not matter.
+    uint32_t d1 = 1u;
+    bool ok1 = true;
+    if (kp.cfg & EV_CFG_DRAWS) {                      // wave-uniform
+      const uint4 w1 = philox(lo, hi, kr, (1u << 24) | (1u << 16) | (p << 8) | a, skey(kp.k0), skey(kp.k1));
+      ok1 = !(lossy && w1.x <= loss_m1);
+      d1 = faulty ? 1u + mulhi_n(w1.y, dmax) : 1u;
+    }
+    msgs += snd1 ? 1u : 0u;
+    bailed = bailed || (snd1 && kr == (S::CMP ? (1u << S::KB) - 1u : 0xFFFFu));
+    if (!S::CMP) m.st16(snd1 ? S::RSEQ : S::DUMMY, snd1 ? L : 0u, kr + 1u);
+    {
+      // enqueue (predicated: inactive lanes store to the dummy word)
+      const bool go = snd1 && ok1;
+      const uint32_t Lr = p * (uint32_t)N + a;
+      const uint32_t rr = rsp_ld(Lr);
+      const uint32_t rlen = (rr >> S::RL) & RLM;
+      bailed = bailed || (go && (rlen >= (uint32_t)S::RC || pfree == 0));
+      const uint32_t rel = rlen ? (((rr >> S::RD) & 15u) - s4) & 15u : 0u;
+      const uint32_t due_rel = d1 > rel ? d1 : rel;
+      const uint32_t due4 = (s4 + due_rel) & 15u;
+      const uint32_t k2 = (POOL > 32) ? (uint32_t)__builtin_ctzll((unsigned long long)pfree | (1ull << 63))
+                                      : ctz32((uint32_t)pfree) & 31u;
+      pfree &= go ? ~((pool_mask_t)1 << k2) : ~(pool_mask_t)0;
+      m.st(go ? S::POOLW + k2 : S::DUMMY, rx | (ry << 12) | (rz << 24) | (due4 << 26) | (rk << 30));
+      m.st(go ? S::RSP + Lr : S::DUMMY, (rr & ((1u << (S::IB * rlen)) - 1u)) | (k2 << (S::IB * rlen)) |
+                                            ((rlen + 1u) << S::RL) | (due4 << S::RD));
+      const uint32_t slot = ((uint32_t)s + due_rel) & WM;
+      m.orw(go ? S::WHEEL + slot * S::WW + (S::WW == 2 ? 1u : 0u) : S::DUMMY, 1u << (S::ISH + p * (N + 1) + 1u + a));
+      occ |= go ? (1u << slot) : 0u;
+      in_flight += go ? 1u : 0u;
+    }
 
-    // ================= PROP: one input of one proposer =================
-    const bool pin = in_mask != 0u && pq_len + 2u <= PQ_CAP;
+  }
+
+  // ================= PROP: one input of one proposer =================
+  __host__ __device__ __forceinline__ bool prop_ready() const { return in_mask != 0u && pq_len + 2u <= PQ_CAP; }
+  __host__ __device__ __forceinline__ void prop_op(const EvParams& kp, bool act) {
+    const uint32_t s4 = (uint32_t)s & 15u;
+    const bool pin = act && in_mask != 0u && pq_len + 2u <= PQ_CAP;
     {
       const uint32_t j = pin ? ctz32(in_mask) : 0u;
       const uint32_t q = j / (uint32_t)(N + 1);
@@ -452,17 +518,14 @@ struct EvLane {
       const bool resp = pin && r != 0u;
       const uint32_t ra = r - 1u;
       const uint32_t Lr = q * (uint32_t)N + (resp ? ra : 0u);
-      const uint32_t rmr = m.ld(S::RSP + Lr);
-      const uint32_t rlen = (rmr >> (4 * S::IB)) & 7u;
-      const uint32_t im = (1u << S::IB) - 1u;
-      const uint32_t k = rmr & im;
+      const uint32_t rr = rsp_ld(Lr);
+      const uint32_t rlen = (rr >> S::RL) & RLM;
+      const uint32_t k = rr & IM;
       const uint32_t pe = m.ld(S::POOLW + k);
-      const uint32_t pn = m.ld(S::POOLW + ((rmr >> S::IB) & im));
-      if (resp) {
-        pfree |= (pool_mask_t)1 << k;
-        m.st(S::RSP + Lr, ((rmr & ((1u << (4 * S::IB)) - 1u)) >> S::IB) | ((rlen - 1u) << (4 * S::IB)) |
-                              (rmr & (15u << (4 * S::IB + 3))));
-      }
+      const uint32_t pn = m.ld(S::POOLW + ((rr >> S::IB) & IM));
+      pfree |= resp ? ((pool_mask_t)1 << k) : (pool_mask_t)0;
+      m.st(resp ? S::RSP + Lr : S::DUMMY, ((rr & ((1u << S::RL) - 1u)) >> S::IB) | ((rlen - 1u) << S::RL) |
+                                              (rr & (15u << S::RD)));
       const bool rkeep = resp && rlen > 1u && ((pn >> 26) & 15u) == s4;
       in_mask = (pin && !rkeep) ? (in_mask & ~(1u << j)) : in_mask;
       in_flight -= resp ? 1u : 0u;
@@ -506,45 +569,12 @@ struct EvLane {
       broadcast(q, k0o, x0o, z0o, k0o != NONE);
       broadcast(q, ASK, Tn, 0u, b1);
     }
-#pragma unroll
-    for (int c = 0; c < PXB_EV_CPOST; ++c) copy_send(kp, s4);
+  }
 
-    // ================= the iteration's sends (SEMANTICS §5) =================
-    // reply on a -> p (Philox seq = the link's reply count)
-    uint32_t d1 = 1u;
-    bool ok1 = true;
-    if (faulty) {
-      const uint4 w1 = philox(lo, hi, kr, (1u << 24) | (1u << 16) | (p << 8) | a, kp.k0, kp.k1);
-      ok1 = !(lossy && w1.x <= loss_m1);
-      d1 = 1u + mulhi_n(w1.y, dmax);
-    }
-    if (snd1) {
-      msgs += 1u;
-      if (kr == 0xFFFFu) bailed = true;
-      m.st16(S::RSEQ, L, kr + 1u);
-    }
-    if (snd1 && ok1) {
-      const uint32_t Lr = p * (uint32_t)N + a;
-      const uint32_t rmr = m.ld(S::RSP + Lr);
-      const uint32_t rlen = (rmr >> (4 * S::IB)) & 7u;
-      if (rlen >= CPHYS || pfree == 0) bailed = true;
-      const uint32_t rel = rlen ? (((rmr >> (4 * S::IB + 3)) & 15u) - s4) & 15u : 0u;
-      const uint32_t due_rel = d1 > rel ? d1 : rel;
-      const uint32_t due4 = (s4 + due_rel) & 15u;
-      const uint32_t k2 = (POOL > 32) ? (uint32_t)__builtin_ctzll((unsigned long long)pfree | (1ull << 63))
-                                      : ctz32((uint32_t)pfree) & 31u;
-      pfree &= ~((pool_mask_t)1 << k2);
-      m.st(S::POOLW + k2, rx | (ry << 12) | (rz << 24) | (due4 << 26) | (rk << 30));
-      m.st(S::RSP + Lr, (rmr & ((1u << (S::IB * rlen)) - 1u)) | (k2 << (S::IB * rlen)) |
-                            ((rlen + 1u) << (4 * S::IB)) | (due4 << (4 * S::IB + 3)));
-      const uint32_t slot = ((uint32_t)s + due_rel) & WM;
-      const uint32_t wi = S::WHEEL + slot * S::WW + (S::WW == 2 ? 1u : 0u);
-      m.orw(wi, 1u << (S::ISH + p * (N + 1) + 1u + a));
-      occ |= 1u << slot;
-      in_flight += 1u;
-    }
-    // ================= END of step: quiescence, step cap, next step =================
-    if (acc_mask == 0u && in_mask == 0u && pq_len == 0u) {
+  // ================= END of step: quiescence, step cap, next step =================
+  __host__ __device__ __forceinline__ bool end_ready() const { return acc_mask == 0u && in_mask == 0u && pq_len == 0u; }
+  __host__ __device__ __forceinline__ bool end_op(const EvParams& kp, EvOut& o, bool act) {
+    if (act && acc_mask == 0u && in_mask == 0u && pq_len == 0u) {
       const bool quiet = in_flight == 0u && s >= last_tick;
       if (quiet) {
         finish(false, o);
@@ -585,7 +615,7 @@ struct EvLane {
   }
 
   // final per-acceptor outputs (digest, record) of an ended instance
-  __host__ __device__ uint32_t digest_of(int a) const { return fnv_u32(m.ld(S::ACCD + a), accw[a] >> 27); }
+  __host__ __device__ uint32_t digest_of(int a) const { return fnv_u32(accd[a], accw[a] >> 27); }
   __host__ __device__ void record_of(int a, uint32_t r[4]) const {
     const uint32_t A = accw[a];
     const uint32_t val = (A >> 24) & 3u;
@@ -625,6 +655,7 @@ __host__ inline EvParams make_params(const pxb_config* c) {
   p.step_cap = c->step_cap;
   const uint64_t lt = ev_threshold(c->loss_ppm), ct = ev_threshold(c->crash_ppm);
   p.cfg = ((c->flags & PXB_CFG_RANDOMIZE) ? EV_CFG_RANDOMIZE : 0u) | (lt ? EV_CFG_LOSSY : 0u) | (ct ? EV_CFG_CRASHY : 0u);
+  if ((c->flags & PXB_CFG_RANDOMIZE) || lt || c->delay_max > 1) p.cfg |= EV_CFG_DRAWS;
   p.loss_m1 = (uint32_t)(lt - 1ull);
   p.crash_m1 = (uint32_t)(ct - 1ull);
   return p;
@@ -632,6 +663,23 @@ __host__ inline EvParams make_params(const pxb_config* c) {
 
 // the timing wheel must outlast the longest delay
 __host__ inline int wheel_for(uint32_t delay_max) { return delay_max <= 7 ? 8 : 16; }
+
+// Kernel layout of a launch: 0 = 8-step wheel, 1 = 16-step wheel, 2 = compact
+// links (3-entry request FIFOs sharing a word with the reply seq, a 24-word
+// response pool, 8-step wheel).  Short delays keep FIFOs short (BASELINE
+// config 4: 0.9 % of instances ever hold a fourth request on one link, config
+// 3: 0.02 %; those are bailed to the general kernel), so they take the compact
+// layout, which fits more resident waves; fuzzed or long-delay schedules keep
+// 4-entry FIFOs.  The compact reply seq has 9 bits (config 4 reaches 68 in 256
+// steps), so long runs keep the separate 16-bit one; three duelling proposers
+// over 9 acceptors overflow the 3-entry FIFOs too often (25 % of instances at
+// 10 % loss), so the compact layout is kept to topologies of <= 16 links.
+__host__ inline int layout_for(const pxb_config* c) {
+  if (!(c->flags & PXB_CFG_RANDOMIZE) && c->delay_max <= 4 && c->step_cap <= 512 &&
+      c->n_proposers * c->n_acceptors <= 16)
+    return 2;
+  return wheel_for(c->delay_max) == 8 ? 0 : 1;
+}
 
 }  // namespace ev
 }  // namespace pxb

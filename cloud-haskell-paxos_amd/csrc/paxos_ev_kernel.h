@@ -1,9 +1,11 @@
 // paxos_ev_kernel.h — gfx950 wave driver of the per-lane kernel (paxos_ev.h).
 //
 // One 64-lane wave per block, persistent: every lane runs its own instance one
-// micro-step per iteration and, when the instance ends (or bails), writes its
+// iteration at a time and, when the instance ends (or bails), writes its
 // outputs and takes the next instance id from the wave's chunk of the launch's
-// work queue.  The per-lane state lives in the block's LDS, lane-interleaved.
+// work queue.  The per-lane state lives in registers and in the block's LDS,
+// lane-interleaved; the block's resident count is set by that LDS (the kernel
+// is latency-bound, so every byte per lane matters: DESIGN.md §3).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -44,16 +46,25 @@ struct EvKParams {
   uint32_t* bail_n;                           // their count, 0 on entry
 };
 
-// pool / wheel sizes of a (PM, N, delay) shape
-template <int PM, int N> struct EvPool { static constexpr int value = (PM * N <= 16) ? 32 : 64; };
+// response-pool words per lane of a shape (the compact layout is picked for
+// schedules with short delays, whose responses in flight stay fewer)
+template <int PM, int N, bool CMP>
+struct EvPool {
+  static constexpr int value = (PM * N <= 16) ? (CMP ? 24 : 32) : (CMP ? 48 : 64);
+};
 
-template <int PM, int N, int W>
+// run totals kept per wave in LDS (added once per finished instance)
+constexpr int EV_NTOT = 11;
+
+template <int PM, int N, int W, bool CMP>
 __global__ __launch_bounds__(64, 1) void paxos_ev_kernel(EvKParams kp) {
-  constexpr int POOL = EvPool<PM, N>::value;
-  using S = Shape<PM, N, POOL, W>;
+  constexpr int POOL = EvPool<PM, N, CMP>::value;
+  using S = Shape<PM, N, POOL, W, CMP>;
   __shared__ uint32_t lds[S::WORDS * 64];
+  __shared__ unsigned long long wtot[16];
   const uint32_t lane = threadIdx.x;
-  EvLane<PM, N, POOL, W, LdsMem> L;
+  if (lane < 16) wtot[lane] = 0ull;
+  EvLane<PM, N, POOL, W, CMP, LdsMem> L;
   L.m = LdsMem{lds, lane};
   L.mode = M_IDLE;
   L.bailed = false;
@@ -61,10 +72,6 @@ __global__ __launch_bounds__(64, 1) void paxos_ev_kernel(EvKParams kp) {
   const uint64_t below = (1ull << lane) - 1ull;
   uint32_t next = 0, end = 0;
   bool drained = false;
-  // lane totals over the instances this lane ran
-  uint32_t t_inst = 0, t_undec = 0, t_stuck = 0, t_panic = 0, t_div = 0, t_cap = 0;
-  uint32_t t_rounds = 0, t_steps = 0, t_msgs = 0, t_execs = 0;
-  unsigned long long t_canon = 0;
 
   for (;;) {
     // ---- refill idle lanes from the wave's chunk of the queue ----
@@ -89,7 +96,7 @@ __global__ __launch_bounds__(64, 1) void paxos_ev_kernel(EvKParams kp) {
     }
     if (__builtin_amdgcn_ballot_w64(L.mode != M_IDLE) == 0ull) break;
 
-    // ---- one micro-step of every live lane ----
+    // ---- one iteration of every live lane ----
     if (L.mode != M_IDLE) {
       EvOut o;
       const bool done = L.step(kp.p, o);
@@ -100,17 +107,20 @@ __global__ __launch_bounds__(64, 1) void paxos_ev_kernel(EvKParams kp) {
         L.bailed = false;
       } else if (done) {
         const uint32_t f = o.flags;
-        t_inst += 1u;
-        t_undec += (f & PXB_F_UNDECIDED) ? 1u : 0u;
-        t_stuck += (f & PXB_F_STUCK) ? 1u : 0u;
-        t_panic += (f & PXB_F_PANIC) ? 1u : 0u;
-        t_div += (f & PXB_F_LOG_DIVERGENCE) ? 1u : 0u;
-        t_cap += (f & PXB_F_STEP_CAP) ? 1u : 0u;
-        t_rounds += L.rounds;
-        t_steps += o.steps;
-        t_msgs += L.msgs;
-        t_execs += L.execs;
-        t_canon += L.canon;
+        const uint32_t v[EV_NTOT] = {1u,
+                                     (f & PXB_F_UNDECIDED) ? 1u : 0u,
+                                     (f & PXB_F_STUCK) ? 1u : 0u,
+                                     (f & PXB_F_PANIC) ? 1u : 0u,
+                                     (f & PXB_F_LOG_DIVERGENCE) ? 1u : 0u,
+                                     (f & PXB_F_STEP_CAP) ? 1u : 0u,
+                                     L.rounds,
+                                     o.steps,
+                                     L.msgs,
+                                     L.execs,
+                                     L.canon};
+#pragma unroll
+        for (int q = 0; q < EV_NTOT; ++q)
+          if (v[q]) atomicAdd(&wtot[q], (unsigned long long)v[q]);
         if (kp.out) kp.out[L.gid] = make_uint4(o.res[0], o.res[1], o.res[2], o.res[3]);
         if (kp.dig) {
 #pragma unroll
@@ -128,29 +138,17 @@ __global__ __launch_bounds__(64, 1) void paxos_ev_kernel(EvKParams kp) {
     }
   }
 
-  // ---- run totals: wave reduction, one atomic per counter into a partial row ----
-  uint32_t v[11] = {t_inst, t_undec, t_stuck, t_panic, t_div, t_cap, t_rounds, t_steps, t_msgs, t_execs,
-                    t_inst - t_undec};
-  unsigned long long c64 = t_canon;
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-#pragma unroll
-    for (int q = 0; q < 11; ++q) v[q] += (uint32_t)__shfl_xor((int)v[q], off);
-    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)c64, off);
-    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(c64 >> 32), off);
-    c64 += ((unsigned long long)hi << 32) | lo;
-  }
+  // ---- run totals: one atomic per counter into a partial row ----
+  __syncthreads();
   unsigned long long* const trow = kp.part + (size_t)(blockIdx.x % EV_TCOPIES) * 16u;
-  if (lane < 11) {
-    const int slot_of[11] = {PXB_C_INSTANCES, PXB_C_UNDECIDED, PXB_C_STUCK, PXB_C_PANIC, PXB_C_DIVERGENCE,
-                             PXB_C_STEP_CAP, PXB_C_ROUNDS, PXB_C_STEPS, PXB_C_MESSAGES, PXB_C_EXECUTES,
-                             PXB_C_DECIDED};
-    unsigned long long val = 0;
-#pragma unroll
-    for (int q = 0; q < 11; ++q) val = (lane == (uint32_t)q) ? (unsigned long long)v[q] : val;
+  if (lane < EV_NTOT) {
+    const int slot_of[EV_NTOT] = {PXB_C_INSTANCES, PXB_C_UNDECIDED, PXB_C_STUCK, PXB_C_PANIC, PXB_C_DIVERGENCE,
+                                  PXB_C_STEP_CAP, PXB_C_ROUNDS, PXB_C_STEPS, PXB_C_MESSAGES, PXB_C_EXECUTES,
+                                  PXB_C_CANON_BYTES};
+    const unsigned long long val = wtot[lane];
     if (val) atomicAdd(&trow[slot_of[lane]], val);
+    if (lane == 0 && wtot[0] != wtot[1]) atomicAdd(&trow[PXB_C_DECIDED], wtot[0] - wtot[1]);
   }
-  if (lane == 11 && c64) atomicAdd(&trow[PXB_C_CANON_BYTES], c64);
 }
 
 }  // namespace ev

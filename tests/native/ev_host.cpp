@@ -4,11 +4,12 @@
 // GPU.  The product runs the same EvLane code on the device
 // (paxos_ev_kernel.h); nothing here is linked into libpaxos_batch.so.
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <vector>
 
-#include "../../cloud-haskell-paxos_amd/csrc/paxos_ev.h"
+#include "../../cloud-haskell-paxos_amd/csrc/paxos_ev_kernel.h"
 
 using namespace pxb;
 using namespace pxb::ev;
@@ -24,14 +25,14 @@ struct HostMem {
   void orw(uint32_t i, uint32_t v) const { w[i] |= v; }
 };
 
-template <int PM, int N, int W>
+template <int PM, int N, int W, bool CMP>
 int run_shape(const pxb_config* cfg, pxb_result* out, uint32_t* dig, pxb_acceptor_rec* acc, int64_t* tot,
               uint32_t* bail_ids, uint32_t* n_bail, uint64_t* micro_steps) {
-  constexpr int POOL = (PM * N <= 16) ? 32 : 64;
-  using S = Shape<PM, N, POOL, W>;
+  constexpr int POOL = EvPool<PM, N, CMP>::value;
+  using S = Shape<PM, N, POOL, W, CMP>;
   std::vector<uint32_t> buf(S::WORDS + 1, 0xDEADBEEFu);   // garbage: init must set what it reads
   const EvParams p = make_params(cfg);
-  EvLane<PM, N, POOL, W, HostMem> L;
+  EvLane<PM, N, POOL, W, CMP, HostMem> L;
   L.m = HostMem{buf.data()};
   uint32_t nb = 0;
   uint64_t ms = 0;
@@ -79,29 +80,29 @@ int run_shape(const pxb_config* cfg, pxb_result* out, uint32_t* dig, pxb_accepto
   return 0;
 }
 
-template <int PM, int W>
+template <int PM, int W, bool CMP>
 int run_n(const pxb_config* c, pxb_result* o, uint32_t* d, pxb_acceptor_rec* a, int64_t* t, uint32_t* b, uint32_t* nb,
           uint64_t* ms) {
   switch (c->n_acceptors) {
-    case 2: return run_shape<PM, 2, W>(c, o, d, a, t, b, nb, ms);
-    case 3: return run_shape<PM, 3, W>(c, o, d, a, t, b, nb, ms);
-    case 4: return run_shape<PM, 4, W>(c, o, d, a, t, b, nb, ms);
-    case 5: return run_shape<PM, 5, W>(c, o, d, a, t, b, nb, ms);
-    case 6: return run_shape<PM, 6, W>(c, o, d, a, t, b, nb, ms);
-    case 7: return run_shape<PM, 7, W>(c, o, d, a, t, b, nb, ms);
-    case 8: return run_shape<PM, 8, W>(c, o, d, a, t, b, nb, ms);
-    case 9: return run_shape<PM, 9, W>(c, o, d, a, t, b, nb, ms);
+    case 2: return run_shape<PM, 2, W, CMP>(c, o, d, a, t, b, nb, ms);
+    case 3: return run_shape<PM, 3, W, CMP>(c, o, d, a, t, b, nb, ms);
+    case 4: return run_shape<PM, 4, W, CMP>(c, o, d, a, t, b, nb, ms);
+    case 5: return run_shape<PM, 5, W, CMP>(c, o, d, a, t, b, nb, ms);
+    case 6: return run_shape<PM, 6, W, CMP>(c, o, d, a, t, b, nb, ms);
+    case 7: return run_shape<PM, 7, W, CMP>(c, o, d, a, t, b, nb, ms);
+    case 8: return run_shape<PM, 8, W, CMP>(c, o, d, a, t, b, nb, ms);
+    case 9: return run_shape<PM, 9, W, CMP>(c, o, d, a, t, b, nb, ms);
   }
   return -1;
 }
 
-template <int W>
+template <int W, bool CMP>
 int run_w(const pxb_config* c, pxb_result* o, uint32_t* d, pxb_acceptor_rec* a, int64_t* t, uint32_t* b, uint32_t* nb,
           uint64_t* ms) {
   switch (c->n_proposers) {
-    case 1: return run_n<1, W>(c, o, d, a, t, b, nb, ms);
-    case 2: return run_n<2, W>(c, o, d, a, t, b, nb, ms);
-    case 3: return run_n<3, W>(c, o, d, a, t, b, nb, ms);
+    case 1: return run_n<1, W, CMP>(c, o, d, a, t, b, nb, ms);
+    case 2: return run_n<2, W, CMP>(c, o, d, a, t, b, nb, ms);
+    case 3: return run_n<3, W, CMP>(c, o, d, a, t, b, nb, ms);
   }
   return -1;
 }
@@ -111,6 +112,14 @@ int run_w(const pxb_config* c, pxb_result* o, uint32_t* d, pxb_acceptor_rec* a, 
 extern "C" int ev_host_run(const pxb_config* cfg, pxb_result* out, uint32_t* dig, pxb_acceptor_rec* acc,
                            int64_t* totals, uint32_t* bail_ids, uint32_t* n_bail, uint64_t* micro_steps) {
   if (!cfg || !eligible(cfg)) return -1;
-  return wheel_for(cfg->delay_max) == 8 ? run_w<8>(cfg, out, dig, acc, totals, bail_ids, n_bail, micro_steps)
-                                        : run_w<16>(cfg, out, dig, acc, totals, bail_ids, n_bail, micro_steps);
+  const char* lv = getenv("EV_LAYOUT");                 // tests: force a layout
+  const int layout = lv ? atoi(lv) : layout_for(cfg);
+  if (layout == 2 && cfg->delay_max > 7) return -1;
+  if (layout == 0 && cfg->delay_max > 7) return -1;
+  switch (layout) {
+    case 0: return run_w<8, false>(cfg, out, dig, acc, totals, bail_ids, n_bail, micro_steps);
+    case 1: return run_w<16, false>(cfg, out, dig, acc, totals, bail_ids, n_bail, micro_steps);
+    case 2: return run_w<8, true>(cfg, out, dig, acc, totals, bail_ids, n_bail, micro_steps);
+  }
+  return -1;
 }
