@@ -76,27 +76,32 @@ __global__ void proposer_hook_kernel(pxb_proposer_rec* st, uint32_t n_acc, const
 
 constexpr uint32_t QWORDS = 4;          // per-slot queue / counter words (finalize_kernel resets them)
 
-// Sums the TCOPIES partial rows into the caller's totals, zeroes them and
-// resets the work queue, so the launch slot is clean for its next use.  One
-// block of TCOPIES threads; thread t reads column t % 16 of rows t/16, t/16+16, ...
-__global__ __launch_bounds__(TCOPIES) void finalize_kernel(unsigned long long* part, uint32_t* queue,
+// Sums the TCOPIES partial rows of the general kernel, and those of the
+// per-lane kernel unless its bailed-id list overflowed (then the general kernel
+// re-ran every instance of the chunk), into the caller's totals; zeroes them
+// and resets the queue words, so the launch slot is clean for its next use.
+// One block of TCOPIES threads; thread t reads column t % 16 of rows t/16,
+// t/16+16, ...  Queue words: [0] the general kernel's work queue, [1] the
+// per-lane kernel's, [2] its bailed-instance count.
+__global__ __launch_bounds__(TCOPIES) void finalize_kernel(unsigned long long* part, unsigned long long* part_ev,
+                                                            uint32_t* queue, uint32_t bail_cap,
                                                             unsigned long long* totals) {
-  // queue words: [0] general kernel's work queue, [1] per-lane kernel's work
-  // queue, [2] its bailed-instance count
   __shared__ unsigned long long acc[16];
   const uint32_t t = threadIdx.x;
   if (t < 16) acc[t] = 0ull;
   __syncthreads();
+  const bool ev_ok = queue[2] <= bail_cap;
   unsigned long long v = 0ull;
 #pragma unroll
   for (uint32_t j = 0; j < 16; ++j) {
-    v += part[t + j * TCOPIES];
+    v += part[t + j * TCOPIES] + (ev_ok ? part_ev[t + j * TCOPIES] : 0ull);
     part[t + j * TCOPIES] = 0ull;
+    part_ev[t + j * TCOPIES] = 0ull;
   }
   if (v) atomicAdd(&acc[t % 16u], v);
   __syncthreads();
   if (t < 16 && acc[t]) atomicAdd(&totals[t], acc[t]);
-  if (t >= 16 && t < 16 + QWORDS && queue) queue[t - 16] = 0u;
+  if (t >= 16 && t < 16 + QWORDS) queue[t - 16] = 0u;
 }
 
 // ---- host side ----------------------------------------------------------------
@@ -181,18 +186,25 @@ static unsigned long long* g_dbg = nullptr;
 static std::mutex g_mu;
 static int g_occ[4][4][10][64];         // [logm*2+ff][pm][n][device] blocks per CU (0 = unknown)
 static int g_cus[64];
-// Per-launch scratch: QSLOTS slots per device, each TCOPIES partial-total rows
-// (16 x u64) + the work-queue counter on its own 128-B line.  Each launch takes
-// the next slot round-robin; its finalize_kernel leaves the slot zeroed, so
+// Per-launch scratch: QSLOTS slots per device, each two sets of TCOPIES
+// partial-total rows (16 x u64; the general kernel's and the per-lane
+// kernel's) + the queue words on their own 128-B line.  Each launch takes the
+// next slot round-robin; its finalize_kernel leaves the slot zeroed, so
 // consecutive launches need no memset.  Up to QSLOTS launches of one device
 // may be in flight at once (on any streams).
 constexpr int QSLOTS = 64;
-constexpr size_t SLOT_U64 = (size_t)TCOPIES * 16 + 16;
+constexpr size_t ROWS_U64 = (size_t)TCOPIES * 16;
+constexpr size_t SLOT_U64 = 2 * ROWS_U64 + 16;
 static unsigned long long* g_slots[64];
 static uint32_t g_qseq[64];
-// per-lane kernel: bailed-id buffer of each scratch slot (lazily allocated),
-// blocks per CU by [wheel][pm][n][device]
-constexpr uint64_t EV_CHUNK = 1ull << 21;
+// Per-lane kernel: one launch per EV_CHUNK instances; its bailed ids go to the
+// slot's list of EV_BAIL_CAP entries (lazily allocated).  Bails are rare
+// (BASELINE configs: <= 1.5 %); a chunk whose list overflows is re-run whole
+// by the general kernel (finalize_kernel then drops the per-lane totals).
+// Big chunks matter: each one ends with a tail (the slowest instances of the
+// last waves, then of the bailed ones on the general kernel).
+constexpr uint64_t EV_CHUNK = 1ull << 24;
+constexpr uint32_t EV_BAIL_CAP = 1u << 20;
 static uint32_t* g_bail[64][QSLOTS];
 static int g_eocc[3][4][10][64];
 
@@ -285,6 +297,10 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
   // bailed instances on the general faulty kernel; PXB_NO_EV=1 forces the latter
   const char* no_ev = getenv("PXB_NO_EV");
   const bool use_ev = !ff && !logm && ev::eligible(cfg) && !(no_ev && atoi(no_ev) > 0);
+  // tests: a smaller bailed-id list, to exercise its overflow path
+  const char* cap_s = getenv("PXB_EV_BAIL_CAP");
+  const uint32_t bail_cap = (cap_s && atoi(cap_s) >= 0) ? std::min<uint32_t>((uint32_t)atoi(cap_s), EV_BAIL_CAP)
+                                                      : EV_BAIL_CAP;
   kernel_fn fn = pick(cfg->n_proposers, cfg->n_acceptors, logm, ff);
   if (!fn) return PXB_E_INVAL;
   const int layout = ev::layout_for(cfg);
@@ -373,7 +389,7 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
   const uint64_t wpb = (uint64_t)fn.wpb;
   // fault-free log mode: 16-bit epochs, so every block's range (static slices:
   // every wave's) stays below 2^16 instances
-  const uint64_t chunk_max = use_ev ? (uint64_t)EV_CHUNK
+  const uint64_t chunk_max = use_ev ? std::min<uint64_t>(EV_CHUNK, (1ull << 30) - 1)
                              : (ff && logm) ? std::min<uint64_t>(resident * wpb * G * 30000ull, resident * 60000ull)
                              : ff ? std::min<uint64_t>(1ull << 31, resident * wpb * G * 30000ull)
                                   : std::min<uint64_t>((1ull << 30) - 1, resident * wpb * G * 60000ull);
@@ -385,18 +401,24 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
     kp.dig = d_log_digest ? d_log_digest + done * cfg->n_acceptors : nullptr;
     kp.acc = d_acc ? reinterpret_cast<uint4*>(d_acc + done * cfg->n_acceptors) : nullptr;
     uint32_t* bail = nullptr;
-    int sidx;
+    unsigned long long* slot = nullptr;
     {
       std::lock_guard<std::mutex> lk(g_mu);
-      sidx = (int)(g_qseq[dev]++ % QSLOTS);
-      unsigned long long* slot = g_slots[dev] + (size_t)sidx * SLOT_U64;
+      const int sidx = (int)(g_qseq[dev]++ % QSLOTS);
+      slot = g_slots[dev] + (size_t)sidx * SLOT_U64;
       kp.part = slot;
-      kp.queue = reinterpret_cast<uint32_t*>(slot + (size_t)TCOPIES * 16);
+      kp.queue = reinterpret_cast<uint32_t*>(slot + 2 * ROWS_U64);
       if (use_ev) {
-        if (!g_bail[dev][sidx]) HIPCHK(hipMalloc(&g_bail[dev][sidx], (size_t)EV_CHUNK * sizeof(uint32_t)));
+        if (!g_bail[dev][sidx]) HIPCHK(hipMalloc(&g_bail[dev][sidx], (size_t)EV_BAIL_CAP * sizeof(uint32_t)));
         bail = g_bail[dev][sidx];
       }
     }
+    // a launch that fails after an earlier one of this chunk has queued leaves
+    // the slot half used: zero it behind the queued work before reporting
+    auto fail = [&](hipError_t e) {
+      (void)hipMemsetAsync(slot, 0, SLOT_U64 * sizeof(unsigned long long), st);
+      return hip_fail(e);
+    };
     if (use_ev) {
       // the per-lane kernel over the chunk, then the general kernel over its bailed ids
       ev::EvKParams ek;
@@ -407,18 +429,20 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
       ek.out = kp.out;
       ek.dig = kp.dig;
       ek.acc = kp.acc;
-      ek.part = kp.part;
+      ek.part = kp.part + ROWS_U64;
       ek.queue = kp.queue + 1;
       ek.bail_ids = bail;
       ek.bail_n = kp.queue + 2;
+      ek.bail_cap = bail_cap;
       const uint64_t eres = (uint64_t)eocc * (uint64_t)cus;
       const unsigned egrid = (unsigned)std::min<uint64_t>((nc + 63) / 64, eres);
       hipLaunchKernelGGL(efn, dim3(egrid), dim3(64), 0, st, ek);
       HIPCHK(hipGetLastError());
       kp.ids = bail;
       kp.n_ids = kp.queue + 2;
+      kp.ids_cap = bail_cap;
       hipLaunchKernelGGL(fn.fn, dim3((unsigned)resident), dim3(64 * fn.wpb), 0, st, kp);
-      HIPCHK(hipGetLastError());
+      if (hipError_t e = hipGetLastError()) return fail(e);
     } else {
       const uint64_t waves_needed = (nc + G - 1) / G;
       const uint64_t blocks_needed = (waves_needed + wpb - 1) / wpb;
@@ -432,8 +456,9 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
       hipLaunchKernelGGL(fn.fn, dim3(grid), dim3(64 * fn.wpb), 0, st, kp);
       HIPCHK(hipGetLastError());
     }
-    hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(TCOPIES), 0, st, kp.part, kp.queue, totals);
-    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(TCOPIES), 0, st, kp.part, kp.part + ROWS_U64, kp.queue,
+                       bail_cap, totals);
+    if (hipError_t e = hipGetLastError()) return fail(e);
   }
   return PXB_OK;
 }

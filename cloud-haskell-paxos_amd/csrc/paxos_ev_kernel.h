@@ -42,8 +42,9 @@ struct EvKParams {
   uint4* acc;                                 // final acceptor records (nullable)
   unsigned long long* part;                   // EV_TCOPIES partial run-total rows
   uint32_t* queue;                            // next instance, 0 on entry
-  uint32_t* bail_ids;                         // ids of bailed instances (capacity n_instances)
-  uint32_t* bail_n;                           // their count, 0 on entry
+  uint32_t* bail_ids;                         // ids of bailed instances (capacity bail_cap)
+  uint32_t* bail_n;                           // their count, 0 on entry (may exceed bail_cap: overflow)
+  uint32_t bail_cap;
 };
 
 // response-pool words per lane of a shape (the compact layout is picked for
@@ -102,7 +103,7 @@ __global__ __launch_bounds__(64, 1) void paxos_ev_kernel(EvKParams kp) {
       const bool done = L.step(kp.p, o);
       if (L.bailed) {                         // beyond this kernel's capacities: re-run by the general kernel
         const uint32_t pos = atomicAdd(kp.bail_n, 1u);
-        kp.bail_ids[pos] = L.gid;
+        if (pos < kp.bail_cap) kp.bail_ids[pos] = L.gid;
         L.mode = M_IDLE;
         L.bailed = false;
       } else if (done) {

@@ -102,9 +102,11 @@ struct KParams {
   uint32_t* queue;                    // faulty kernels: next instance, 0 on entry
   unsigned long long* dbg;            // diagnostic builds only (PXB_STAMPS)
   // faulty kernels only: run the instances listed in ids[0 .. *n_ids) (the
-  // per-lane kernel's bailed instances, paxos_ev.h) instead of 0 .. n_instances
+  // per-lane kernel's bailed instances, paxos_ev.h) instead of 0 .. n_instances;
+  // a count above ids_cap means the list overflowed: run every instance
   const uint32_t* ids;
   const uint32_t* n_ids;
+  uint32_t ids_cap;
 };
 
 __host__ __device__ inline uint64_t prob_threshold(uint32_t ppm) {
@@ -312,7 +314,9 @@ __global__ __launch_bounds__((Shape<PM, N, LOGM, FF>::block), (Occ<PM, FF>::wave
   const uint32_t nwaves = gridDim.x * WPB;
   // faulty kernels may take their instances from a device-side list (its
   // length is written by the kernel launched before this one)
-  const uint32_t n = (!FF && kp.n_ids) ? (uint32_t)__builtin_amdgcn_readfirstlane((int)*kp.n_ids) : kp.n_instances;
+  const uint32_t n_listed = (!FF && kp.n_ids) ? (uint32_t)__builtin_amdgcn_readfirstlane((int)*kp.n_ids) : 0u;
+  const bool listed = !FF && kp.n_ids && n_listed <= kp.ids_cap;
+  const uint32_t n = listed ? n_listed : kp.n_instances;
   // faulty kernels: chunks from the device work queue (DYN); fault-free
   // kernels: one-generation chunks of the block's contiguous range from an
   // LDS counter (BQ); diagnostic builds: a static slice per wave
@@ -556,7 +560,7 @@ __global__ __launch_bounds__((Shape<PM, N, LOGM, FF>::block), (Occ<PM, FF>::wave
       const uint32_t cand = next + (uint32_t)__popcll(freeb & ((1ull << base) - 1ull));
       if (used && !active && cand < end) {
         idx = cand;
-        gid = (!FF && kp.ids) ? kp.ids[cand] : cand;
+        gid = listed ? kp.ids[cand] : cand;
         const uint64_t inst = kp.first_instance + gid;
         const uint32_t ilo = (uint32_t)inst, ihi = (uint32_t)(inst >> 32);
         P = kp.n_prop;

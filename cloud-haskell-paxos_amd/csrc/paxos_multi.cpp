@@ -1,45 +1,180 @@
 // paxos_multi.cpp — multi-GPU entry of the C ABI (pxb_run_multi).
 //
-// One host thread per device runs the device's contiguous share of the global
-// instance range (instances share no state — Main.hs:41-45,
+// Each device runs its contiguous share of the global instance range on its own
+// host thread (instances share no state — Main.hs:41-45,
 // Server.hs:58-71 — and every Philox draw is keyed by the GLOBAL instance id,
 // so results do not depend on the device count).  The only collective is one
-// RCCL all-reduce (sum, int64 x PXB_NCOUNTERS) of the run totals over xGMI,
-// issued once per run by every device thread on its own communicator.
+// RCCL all-reduce (sum, int64 x PXB_NCOUNTERS) of the run totals over xGMI.
+// shard_runner.h orders the phases so that the collective is issued for all
+// devices together (one RCCL group from one thread) or not at all: a device
+// that fails never leaves the others blocked in the all-reduce.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <mutex>
 #include <string.h>
-#include <thread>
+#include <string>
 #include <vector>
 
 #include "../../include/paxos_batch.h"
+#include "shard_runner.h"
 
 namespace {
 
 std::mutex g_comm_mu;
-std::vector<ncclComm_t> g_comms;   // cached communicator set for devices 0..n-1
+std::vector<ncclComm_t> g_comms;   // cached communicators ...
+std::string g_comm_key;            // ... for this device list (PCI bus ids)
 
-int comms_for(int n, std::vector<ncclComm_t>& out) {
+std::string device_key(int G) {
+  std::string key;
+  for (int g = 0; g < G; ++g) {
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof(bus), g) != hipSuccess) snprintf(bus, sizeof(bus), "dev%d", g);
+    key += bus;
+    key += ';';
+  }
+  return key;
+}
+
+void release_locked() {
+  for (ncclComm_t c : g_comms)
+    if (c) ncclCommDestroy(c);
+  g_comms.clear();
+  g_comm_key.clear();
+}
+
+int comms_for(int G, std::vector<ncclComm_t>& out) {
   std::lock_guard<std::mutex> lk(g_comm_mu);
-  if ((int)g_comms.size() != n) {
-    for (ncclComm_t c : g_comms) ncclCommDestroy(c);
-    g_comms.assign(n, nullptr);
-    std::vector<int> devs(n);
-    for (int i = 0; i < n; ++i) devs[i] = i;
-    if (ncclCommInitAll(g_comms.data(), n, devs.data()) != ncclSuccess) {
+  const std::string key = device_key(G);
+  if (key != g_comm_key) {
+    release_locked();
+    g_comms.assign(G, nullptr);
+    std::vector<int> devs(G);
+    for (int i = 0; i < G; ++i) devs[i] = i;
+    if (ncclCommInitAll(g_comms.data(), G, devs.data()) != ncclSuccess) {
       g_comms.clear();
       return PXB_E_RCCL;
     }
+    g_comm_key = key;
   }
   out = g_comms;
   return PXB_OK;
 }
 
+// after a failed collective the communicators may hold half-issued work: abort
+// and forget them (the next call builds new ones)
+void abort_comms() {
+  std::lock_guard<std::mutex> lk(g_comm_mu);
+  for (ncclComm_t c : g_comms)
+    if (c) ncclCommAbort(c);
+  g_comms.clear();
+  g_comm_key.clear();
+}
+
+// tests: make device `g` fail in a phase ("setup" / "compute"), to check that
+// the call returns the error promptly instead of hanging in the collective
+bool injected(const char* phase, int g) {
+  const char* p = getenv("PXB_MULTI_FAIL_PHASE");
+  const char* d = getenv("PXB_MULTI_FAIL_DEVICE");
+  return p && d && strcmp(p, phase) == 0 && atoi(d) == g;
+}
+
+struct HipShards {
+  const pxb_config* cfg;
+  int G;
+  pxb_result* out;
+  uint32_t* log_digest;
+  pxb_acceptor_rec* acc;
+  std::vector<ncclComm_t> comms;
+  struct Dev {
+    hipStream_t st = nullptr;
+    pxb_result* d_out = nullptr;
+    uint32_t* d_dig = nullptr;
+    pxb_acceptor_rec* d_acc = nullptr;
+    int64_t* d_tot = nullptr;
+    uint64_t lo = 0, m = 0;
+    int64_t tot[PXB_NCOUNTERS];
+  };
+  std::vector<Dev> dv;
+
+  int setup(int g) {
+    Dev& d = dv[g];
+    const uint64_t n = cfg->n_instances, N = cfg->n_acceptors;
+    d.lo = n * (uint64_t)g / (uint64_t)G;
+    d.m = n * (uint64_t)(g + 1) / (uint64_t)G - d.lo;
+    if (injected("setup", g)) return PXB_E_HIP;
+    if (hipSetDevice(g) != hipSuccess || hipStreamCreate(&d.st) != hipSuccess) return PXB_E_HIP;
+    if (hipMalloc(&d.d_tot, PXB_NCOUNTERS * sizeof(int64_t)) != hipSuccess) return PXB_E_OOM;
+    if (out && d.m && hipMalloc(&d.d_out, d.m * sizeof(pxb_result)) != hipSuccess) return PXB_E_OOM;
+    if (log_digest && d.m && hipMalloc(&d.d_dig, d.m * N * sizeof(uint32_t)) != hipSuccess) return PXB_E_OOM;
+    if (acc && d.m && hipMalloc(&d.d_acc, d.m * N * sizeof(pxb_acceptor_rec)) != hipSuccess) return PXB_E_OOM;
+    if (hipMemsetAsync(d.d_tot, 0, PXB_NCOUNTERS * sizeof(int64_t), d.st) != hipSuccess) return PXB_E_HIP;
+    return PXB_OK;
+  }
+
+  int compute(int g) {
+    Dev& d = dv[g];
+    if (injected("compute", g)) return PXB_E_HIP;
+    if (hipSetDevice(g) != hipSuccess) return PXB_E_HIP;
+    pxb_config c = *cfg;
+    c.first_instance = cfg->first_instance + d.lo;
+    c.n_instances = d.m;
+    if (int r = pxb_run_device(&c, d.d_out, d.d_dig, d.d_acc, d.d_tot, d.st)) return r;
+    if (hipStreamSynchronize(d.st) != hipSuccess) return PXB_E_HIP;
+    const uint64_t N = cfg->n_acceptors;
+    if (out && d.m && hipMemcpy(out + d.lo, d.d_out, d.m * sizeof(pxb_result), hipMemcpyDeviceToHost) != hipSuccess)
+      return PXB_E_HIP;
+    if (log_digest && d.m &&
+        hipMemcpy(log_digest + d.lo * N, d.d_dig, d.m * N * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
+      return PXB_E_HIP;
+    if (acc && d.m &&
+        hipMemcpy(acc + d.lo * N, d.d_acc, d.m * N * sizeof(pxb_acceptor_rec), hipMemcpyDeviceToHost) != hipSuccess)
+      return PXB_E_HIP;
+    return PXB_OK;
+  }
+
+  // the run's one collective, issued for every device in one group
+  int reduce_all() {
+    if (ncclGroupStart() != ncclSuccess) return PXB_E_RCCL;
+    bool ok = true;
+    for (int g = 0; g < G; ++g)
+      ok = ok && ncclAllReduce(dv[g].d_tot, dv[g].d_tot, PXB_NCOUNTERS, ncclInt64, ncclSum, comms[g], dv[g].st) ==
+                     ncclSuccess;
+    if (ncclGroupEnd() != ncclSuccess || !ok) return PXB_E_RCCL;
+    return PXB_OK;
+  }
+  void abort_reduce() { abort_comms(); }
+
+  int fetch(int g) {
+    Dev& d = dv[g];
+    if (hipSetDevice(g) != hipSuccess || hipStreamSynchronize(d.st) != hipSuccess) return PXB_E_HIP;
+    if (hipMemcpy(d.tot, d.d_tot, PXB_NCOUNTERS * sizeof(int64_t), hipMemcpyDeviceToHost) != hipSuccess)
+      return PXB_E_HIP;
+    return PXB_OK;
+  }
+
+  void teardown(int g) {
+    Dev& d = dv[g];
+    (void)hipSetDevice(g);
+    if (d.st) (void)hipStreamSynchronize(d.st);
+    if (d.d_out) (void)hipFree(d.d_out);
+    if (d.d_dig) (void)hipFree(d.d_dig);
+    if (d.d_acc) (void)hipFree(d.d_acc);
+    if (d.d_tot) (void)hipFree(d.d_tot);
+    if (d.st) (void)hipStreamDestroy(d.st);
+    d = Dev();
+  }
+};
+
 }  // namespace
 
 extern "C" {
+
+// internal (pxb_shutdown): destroy the cached communicators
+void pxb_multi_release(void) {
+  std::lock_guard<std::mutex> lk(g_comm_mu);
+  release_locked();
+}
 
 // Same outputs as pxb_run (host buffers, all nullable) for a batch sharded over
 // devices 0..n_devices-1 (n_devices <= 0: every visible device).  totals are the
@@ -51,63 +186,14 @@ int pxb_run_multi(const pxb_config* cfg, int n_devices, pxb_result* out, uint32_
   if (hipGetDeviceCount(&visible) != hipSuccess || visible == 0) return PXB_E_NODEV;
   const int G = (n_devices <= 0) ? visible : n_devices;
   if (G > visible) return PXB_E_INVAL;
-  std::vector<ncclComm_t> comms;
-  int rc = comms_for(G, comms);
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  HipShards b{cfg, G, out, log_digest, acc, {}, std::vector<HipShards::Dev>(G)};
+  if (int rc = comms_for(G, b.comms)) return rc;
+  const int rc = pxb::run_shards(b, G);
+  (void)hipSetDevice(cur);
   if (rc) return rc;
-  const uint64_t n = cfg->n_instances, N = cfg->n_acceptors;
-  std::vector<int> rcs(G, PXB_OK);
-  std::vector<int64_t> host_tot((size_t)G * PXB_NCOUNTERS, 0);
-  std::vector<std::thread> th;
-  for (int g = 0; g < G; ++g) {
-    th.emplace_back([&, g]() {
-      const uint64_t lo = n * (uint64_t)g / (uint64_t)G, hi = n * (uint64_t)(g + 1) / (uint64_t)G;
-      pxb_config c = *cfg;
-      c.first_instance = cfg->first_instance + lo;
-      c.n_instances = hi - lo;
-      int r = PXB_OK;
-      pxb_result* d_out = nullptr;
-      uint32_t* d_dig = nullptr;
-      pxb_acceptor_rec* d_acc = nullptr;
-      int64_t* d_tot = nullptr;
-      hipStream_t st = nullptr;
-      do {
-        if (hipSetDevice(g) != hipSuccess || hipStreamCreate(&st) != hipSuccess) { r = PXB_E_HIP; break; }
-        if (hipMalloc(&d_tot, PXB_NCOUNTERS * sizeof(int64_t)) != hipSuccess) { r = PXB_E_OOM; break; }
-        const uint64_t m = c.n_instances;
-        if (out && m && hipMalloc(&d_out, m * sizeof(pxb_result)) != hipSuccess) { r = PXB_E_OOM; break; }
-        if (log_digest && m && hipMalloc(&d_dig, m * N * sizeof(uint32_t)) != hipSuccess) { r = PXB_E_OOM; break; }
-        if (acc && m && hipMalloc(&d_acc, m * N * sizeof(pxb_acceptor_rec)) != hipSuccess) { r = PXB_E_OOM; break; }
-        if (hipMemsetAsync(d_tot, 0, PXB_NCOUNTERS * sizeof(int64_t), st) != hipSuccess) { r = PXB_E_HIP; break; }
-        r = pxb_run_device(&c, d_out, d_dig, d_acc, d_tot, st);
-        if (r) break;
-        if (hipStreamSynchronize(st) != hipSuccess) { r = PXB_E_HIP; break; }
-        if (out && m && hipMemcpy(out + lo, d_out, m * sizeof(pxb_result), hipMemcpyDeviceToHost) != hipSuccess) { r = PXB_E_HIP; break; }
-        if (log_digest && m &&
-            hipMemcpy(log_digest + lo * N, d_dig, m * N * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess) { r = PXB_E_HIP; break; }
-        if (acc && m &&
-            hipMemcpy(acc + lo * N, d_acc, m * N * sizeof(pxb_acceptor_rec), hipMemcpyDeviceToHost) != hipSuccess) { r = PXB_E_HIP; break; }
-      } while (0);
-      rcs[g] = r;
-      // the run's one collective: every device joins it (with zeros on failure)
-      if (d_tot && st) {
-        if (ncclAllReduce(d_tot, d_tot, PXB_NCOUNTERS, ncclInt64, ncclSum, comms[g], st) != ncclSuccess)
-          rcs[g] = PXB_E_RCCL;
-        else if (hipStreamSynchronize(st) != hipSuccess ||
-                 hipMemcpy(&host_tot[(size_t)g * PXB_NCOUNTERS], d_tot, PXB_NCOUNTERS * sizeof(int64_t),
-                           hipMemcpyDeviceToHost) != hipSuccess)
-          rcs[g] = PXB_E_HIP;
-      }
-      if (d_out) (void)hipFree(d_out);
-      if (d_dig) (void)hipFree(d_dig);
-      if (d_acc) (void)hipFree(d_acc);
-      if (d_tot) (void)hipFree(d_tot);
-      if (st) (void)hipStreamDestroy(st);
-    });
-  }
-  for (auto& t : th) t.join();
-  for (int g = 0; g < G; ++g)
-    if (rcs[g]) return rcs[g];
-  if (totals) memcpy(totals->c, host_tot.data(), PXB_NCOUNTERS * sizeof(int64_t));   // rank 0's reduced copy
+  if (totals) memcpy(totals->c, b.dv[0].tot, PXB_NCOUNTERS * sizeof(int64_t));   // the reduced totals
   return PXB_OK;
 }
 

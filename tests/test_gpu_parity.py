@@ -176,6 +176,54 @@ def test_config3_full_size_sampled(gpu_lib):
         assert np.array_equal(res[i], eres[0]) and np.array_equal(dig[i], edig[0])
 
 
+def test_config5_per_gpu_share_sampled(gpu_lib):
+    """BASELINE config 5 at its per-GPU share (2^28 over 8 GPUs = 2^25
+    instances in one call): totals equal the per-instance flags, and a random
+    sample of 64 instances matches the oracle bit-exact."""
+    cfg = pxb.CONFIGS[5]
+    n = pxb.CONFIG_INSTANCES[5] // 8
+    res, dig, _, cnt = pxb.run(cfg, 0, n)
+    assert cnt["instances"] == n and cnt["decided"] + cnt["undecided"] == n
+    flags = res[:, 3] & 0xFF
+    for key, bit in (("undecided", pxb.F_UNDECIDED), ("stuck", pxb.F_STUCK), ("panic", pxb.F_PANIC),
+                     ("divergence", pxb.F_LOG_DIVERGENCE), ("step_cap", pxb.F_STEP_CAP)):
+        assert cnt[key] == int(((flags & bit) != 0).sum()), key
+    assert cnt["rounds"] == int(res[:, 2].astype(np.int64).sum())
+    assert cnt["steps"] == int((res[:, 3] >> 16).astype(np.int64).sum())
+    rng = np.random.default_rng(55)
+    for i in rng.choice(n, 64, replace=False):
+        eres, edig, _, _ = oracle_c.run_cpu(cfg, int(i), 1)
+        assert np.array_equal(res[i], eres[0]) and np.array_equal(dig[i], edig[0])
+
+
+@pytest.mark.parametrize("cap", [0, 3, 1 << 20])
+def test_per_lane_bail_list_overflow(gpu_lib, cap):
+    """Instances the per-lane kernel cannot hold go to a capped id list for the
+    general kernel; when the list overflows, the general kernel re-runs the
+    whole chunk and the per-lane totals are dropped.  Results and totals stay
+    exact either way (config 4 bails ~1.4 % of instances)."""
+    os.environ["PXB_EV_BAIL_CAP"] = str(cap)
+    try:
+        _cmp(pxb.CONFIGS[4], 1 << 30, 30000)
+    finally:
+        del os.environ["PXB_EV_BAIL_CAP"]
+
+
+def test_per_lane_matches_general_kernel(gpu_lib):
+    """The per-lane kernel (default for faulty single-decree batches) and the
+    general kernel (PXB_NO_EV=1) give identical results, digests and totals."""
+    cfg = pxb.CONFIGS[4]
+    a = pxb.run(cfg, 777, 50000, want_acceptors=True)
+    os.environ["PXB_NO_EV"] = "1"
+    try:
+        b = pxb.run(cfg, 777, 50000, want_acceptors=True)
+    finally:
+        del os.environ["PXB_NO_EV"]
+    for x, y in zip(a[:3], b[:3]):
+        assert np.array_equal(x, y)
+    assert a[3] == b[3]
+
+
 def test_device_entry_accumulates_totals(gpu_lib):
     import torch
     cfg = pxb.CONFIGS[3]
