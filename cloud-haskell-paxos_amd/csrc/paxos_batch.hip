@@ -204,6 +204,7 @@ static uint32_t g_qseq[64];
 // Big chunks matter: each one ends with a tail (the slowest instances of the
 // last waves, then of the bailed ones on the general kernel).
 constexpr uint64_t EV_CHUNK = 1ull << 24;
+constexpr int EV_MIN_BLOCKS = 6;
 constexpr uint32_t EV_BAIL_CAP = 1u << 20;
 static uint32_t* g_bail[64][QSLOTS];
 static int g_eocc[3][4][10][64];
@@ -265,6 +266,70 @@ int pxb_debug_wave_times(unsigned long long* out, unsigned max_waves) {
 #endif
 int pxb_last_hip_error(void) { return g_last_hip; }
 
+// per-device scratch of pxb_run_device (callers hold g_mu)
+static int ensure_slots(int dev) {
+  if (g_slots[dev]) return PXB_OK;
+  unsigned long long* q = nullptr;
+  HIPCHK(hipMalloc(&q, QSLOTS * SLOT_U64 * sizeof(unsigned long long)));
+  HIPCHK(hipMemset(q, 0, QSLOTS * SLOT_U64 * sizeof(unsigned long long)));
+  HIPCHK(hipDeviceSynchronize());
+  g_slots[dev] = q;
+  return PXB_OK;
+}
+
+extern "C" void pxb_multi_release(void);   // paxos_multi.cpp
+extern "C" void pxb_wire_release(void);    // paxos_wire.hip
+
+int pxb_init(int n_devices) {
+  int visible = 0;
+  if (hipGetDeviceCount(&visible) != hipSuccess || visible == 0) return PXB_E_NODEV;
+  const int G = (n_devices <= 0) ? visible : n_devices;
+  if (G > visible || G > 64) return PXB_E_INVAL;
+  int cur = 0;
+  HIPCHK(hipGetDevice(&cur));
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (int d = 0; d < G; ++d) {
+    HIPCHK(hipSetDevice(d));
+    if (int rc = ensure_slots(d)) {
+      (void)hipSetDevice(cur);
+      return rc;
+    }
+    if (!g_cus[d]) {
+      hipDeviceProp_t prop;
+      HIPCHK(hipGetDeviceProperties(&prop, d));
+      g_cus[d] = prop.multiProcessorCount;
+    }
+  }
+  HIPCHK(hipSetDevice(cur));
+  return PXB_OK;
+}
+
+int pxb_shutdown(void) {
+  int cur = 0;
+  const bool have_dev = hipGetDevice(&cur) == hipSuccess;
+  int rc = PXB_OK;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    for (int d = 0; d < 64; ++d) {
+      bool any = g_slots[d] != nullptr;
+      for (int k = 0; k < QSLOTS; ++k) any = any || g_bail[d][k] != nullptr;
+      if (!any) continue;
+      if (hipSetDevice(d) != hipSuccess || hipDeviceSynchronize() != hipSuccess) rc = PXB_E_HIP;
+      if (g_slots[d]) (void)hipFree(g_slots[d]);
+      g_slots[d] = nullptr;
+      for (int k = 0; k < QSLOTS; ++k) {
+        if (g_bail[d][k]) (void)hipFree(g_bail[d][k]);
+        g_bail[d][k] = nullptr;
+      }
+      g_qseq[d] = 0;
+    }
+  }
+  pxb_multi_release();
+  pxb_wire_release();
+  if (have_dev) (void)hipSetDevice(cur);
+  return rc;
+}
+
 const char* pxb_strerror(int code) {
   switch (code) {
     case PXB_OK: return "ok";
@@ -294,9 +359,14 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
   const bool ff = !(cfg->flags & PXB_CFG_RANDOMIZE) && cfg->loss_ppm == 0 && cfg->delay_max == 1 &&
                   cfg->crash_ppm == 0;
   // faulty single-decree batches run on the per-lane kernel (paxos_ev.h), its
-  // bailed instances on the general faulty kernel; PXB_NO_EV=1 forces the latter
+  // bailed instances on the general faulty kernel, unless the per-lane layout
+  // of the topology leaves fewer than EV_MIN_BLOCKS resident waves per CU (it
+  // is latency-bound: measured 8.8 / 17.5 / 23.9 M instances/s on config 4 at
+  // 2 / 4 / 6 waves, and the P = 3, N = 9, 16-step layout fits only 3).
+  // PXB_NO_EV=1 forces the general kernel, PXB_FORCE_EV=1 the per-lane one.
   const char* no_ev = getenv("PXB_NO_EV");
-  const bool use_ev = !ff && !logm && ev::eligible(cfg) && !(no_ev && atoi(no_ev) > 0);
+  const char* force_ev = getenv("PXB_FORCE_EV");
+  bool use_ev = !ff && !logm && ev::eligible(cfg) && !(no_ev && atoi(no_ev) > 0);
   // tests: a smaller bailed-id list, to exercise its overflow path
   const char* cap_s = getenv("PXB_EV_BAIL_CAP");
   const uint32_t bail_cap = (cap_s && atoi(cap_s) >= 0) ? std::min<uint32_t>((uint32_t)atoi(cap_s), EV_BAIL_CAP)
@@ -335,14 +405,9 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
         eo = std::max(1, nb);
       }
       eocc = eo;
+      if (eocc < EV_MIN_BLOCKS && !(force_ev && atoi(force_ev) > 0)) use_ev = false;
     }
-    if (!g_slots[dev]) {
-      unsigned long long* q = nullptr;
-      HIPCHK(hipMalloc(&q, QSLOTS * SLOT_U64 * sizeof(unsigned long long)));
-      HIPCHK(hipMemset(q, 0, QSLOTS * SLOT_U64 * sizeof(unsigned long long)));
-      HIPCHK(hipDeviceSynchronize());
-      g_slots[dev] = q;
-    }
+    if (int rc2 = ensure_slots(dev)) return rc2;
     const char* cap_env = getenv("PXB_BLOCKS_PER_CU");   // tests / experiments: cap residency
     if (cap_env && atoi(cap_env) > 0) {
       occ = std::min(occ, atoi(cap_env));

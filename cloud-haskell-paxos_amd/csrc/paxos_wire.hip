@@ -292,7 +292,7 @@ __device__ __forceinline__ uint32_t decode_record(In& r, uint32_t type, pxb_msg&
 // the range is loaded with aligned 16-B loads into LDS and each record parsed
 // from there; any record outside that range (or a tile with malformed
 // offsets) is parsed straight from HBM.
-__global__ __launch_bounds__(DTILE) void decode_kernel(const uint8_t* __restrict__ bytes,
+__global__ __launch_bounds__(DTILE) void decode_kernel(const uint8_t* __restrict__ bytes, uint64_t nbytes,
                                                       const uint64_t* __restrict__ offs, uint64_t n, uint32_t type,
                                                       pxb_msg* __restrict__ msgs, uint32_t* __restrict__ status) {
   __shared__ uint4 s_buf[Stage<DTILE>::n];
@@ -300,7 +300,7 @@ __global__ __launch_bounds__(DTILE) void decode_kernel(const uint8_t* __restrict
   const uint64_t first = (uint64_t)blockIdx.x * DTILE;
   const uint64_t last = min(first + (uint64_t)DTILE, n);
   const uint64_t lo = offs[first], hi = offs[last];
-  const bool staged = hi >= lo && hi - lo <= (uint64_t)DTILE * PXB_WIRE_MAX_BYTES;
+  const bool staged = hi >= lo && hi <= nbytes && hi - lo <= (uint64_t)DTILE * PXB_WIRE_MAX_BYTES;
   const uint8_t* gsrc = bytes + lo;
   const uint32_t pad = (uint32_t)((uintptr_t)gsrc & 15u);   // LDS byte k <-> global gsrc - pad + k
   if (staged) {
@@ -323,7 +323,10 @@ __global__ __launch_bounds__(DTILE) void decode_kernel(const uint8_t* __restrict
   const uint64_t ee = (e >= b) ? e : b;
   pxb_msg m;
   uint32_t err;
-  if (staged && b >= lo && ee <= hi) {
+  if (ee > nbytes) {                       // the record reaches past the buffer
+    m = pxb_msg{0, 0, 0, 0};
+    err = PXB_WIRE_E_LENGTH;
+  } else if (staged && b >= lo && ee <= hi) {
     const uint8_t* p = buf + pad + (uint32_t)(b - lo);
     In r{p, p + (uint32_t)(ee - b), 0u};
     err = decode_record(r, type, m);
@@ -361,6 +364,22 @@ int scratch(int dev, size_t need) {
 using namespace pxw;
 
 extern "C" {
+
+// internal (pxb_shutdown): free the per-device scan scratch
+void pxb_wire_release(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  int cur = 0;
+  const bool have = hipGetDevice(&cur) == hipSuccess;
+  for (int d = 0; d < 64; ++d) {
+    if (!g_tmp[d]) continue;
+    (void)hipSetDevice(d);
+    (void)hipDeviceSynchronize();
+    (void)hipFree(g_tmp[d]);
+    g_tmp[d] = nullptr;
+    g_tmp_bytes[d] = 0;
+  }
+  if (have) (void)hipSetDevice(cur);
+}
 
 int pxb_wire_size(const pxb_msg* d_msgs, uint64_t count, uint32_t type, uint64_t* d_offsets, void* stream) {
   if (type > PXB_WIRE_RESPONSE || !d_offsets || (count && !d_msgs) || count > (1ull << 40)) return PXB_E_INVAL;
@@ -422,13 +441,13 @@ int pxb_wire_encode_all(const pxb_msg* d_msgs, uint64_t count, uint32_t type, ui
   return (hipGetLastError() == hipSuccess) ? PXB_OK : PXB_E_HIP;
 }
 
-int pxb_wire_decode(const uint8_t* d_bytes, const uint64_t* d_offsets, uint64_t count, uint32_t type,
-                    pxb_msg* d_msgs, uint32_t* d_status, void* stream) {
+int pxb_wire_decode(const uint8_t* d_bytes, uint64_t n_bytes, const uint64_t* d_offsets, uint64_t count,
+                    uint32_t type, pxb_msg* d_msgs, uint32_t* d_status, void* stream) {
   if (type > PXB_WIRE_RESPONSE || count > (1ull << 40)) return PXB_E_INVAL;
   if (count == 0) return PXB_OK;
-  if (!d_offsets || !d_msgs || !d_bytes) return PXB_E_INVAL;
-  hipLaunchKernelGGL(decode_kernel, dim3(tiles_of(count, DTILE)), dim3(DTILE), 0, (hipStream_t)stream, d_bytes, d_offsets,
-                     count, type, d_msgs, d_status);
+  if (!d_offsets || !d_msgs || (n_bytes && !d_bytes)) return PXB_E_INVAL;
+  hipLaunchKernelGGL(decode_kernel, dim3(tiles_of(count, DTILE)), dim3(DTILE), 0, (hipStream_t)stream, d_bytes, n_bytes,
+                     d_offsets, count, type, d_msgs, d_status);
   return (hipGetLastError() == hipSuccess) ? PXB_OK : PXB_E_HIP;
 }
 
@@ -460,14 +479,15 @@ int pxb_wire_encode_host(const pxb_msg* msgs, uint64_t count, uint32_t type, uin
   return rc;
 }
 
-int pxb_wire_decode_host(const uint8_t* in, const uint64_t* offsets, uint64_t count, uint32_t type, pxb_msg* msgs,
-                         uint32_t* status) {
-  if (type > PXB_WIRE_RESPONSE || !offsets || (count && (!in || !msgs))) return PXB_E_INVAL;
+int pxb_wire_decode_host(const uint8_t* in, uint64_t n_bytes, const uint64_t* offsets, uint64_t count, uint32_t type,
+                         pxb_msg* msgs, uint32_t* status) {
+  if (type > PXB_WIRE_RESPONSE || !offsets || (count && !msgs) || (n_bytes && !in)) return PXB_E_INVAL;
   if (count == 0) return PXB_OK;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return PXB_E_NODEV;
-  uint64_t nb = 0;                                       // bytes the offsets can reach
+  uint64_t nb = 0;                                       // bytes the offsets reach inside the buffer
   for (uint64_t k = 0; k <= count; ++k) nb = (offsets[k] > nb) ? offsets[k] : nb;
+  nb = (nb < n_bytes) ? nb : n_bytes;
   pxb_msg* d_m = nullptr;
   uint64_t* d_o = nullptr;
   uint8_t* d_b = nullptr;
@@ -481,7 +501,7 @@ int pxb_wire_decode_host(const uint8_t* in, const uint64_t* offsets, uint64_t co
     if (status && (e = hipMalloc(&d_s, count * sizeof(uint32_t))) != hipSuccess) break;
     if ((e = hipMemcpy(d_o, offsets, (count + 1) * sizeof(uint64_t), hipMemcpyHostToDevice)) != hipSuccess) break;
     if (nb && (e = hipMemcpy(d_b, in, nb, hipMemcpyHostToDevice)) != hipSuccess) break;
-    if ((rc = pxb_wire_decode(d_b, d_o, count, type, d_m, d_s, nullptr)) != PXB_OK) break;
+    if ((rc = pxb_wire_decode(d_b, nb, d_o, count, type, d_m, d_s, nullptr)) != PXB_OK) break;
     if ((e = hipMemcpy(msgs, d_m, count * sizeof(pxb_msg), hipMemcpyDeviceToHost)) != hipSuccess) break;
     if (status && (e = hipMemcpy(status, d_s, count * sizeof(uint32_t), hipMemcpyDeviceToHost)) != hipSuccess) break;
   } while (0);

@@ -44,7 +44,7 @@ data WireError = WireLength | WireTag | WireString | WireRange | WireOther Word3
 foreign import ccall safe "pxb_wire_encode_host"
   c_encode :: Ptr Word32 -> Word64 -> Word32 -> Ptr Word8 -> Ptr Word64 -> Ptr Word64 -> IO CInt
 foreign import ccall safe "pxb_wire_decode_host"
-  c_decode :: Ptr Word8 -> Ptr Word64 -> Word64 -> Word32 -> Ptr Word32 -> Ptr Word32 -> IO CInt
+  c_decode :: Ptr Word8 -> Word64 -> Ptr Word64 -> Word64 -> Word32 -> Ptr Word32 -> Ptr Word32 -> IO CInt
 
 wireRequest, wireResponse, maxBytes :: Word32
 wireRequest = 0
@@ -130,7 +130,7 @@ decodeWith ty conv bytes offsets = do
         allocaArray (4 * n) $ \pm ->
           allocaArray n $ \pst -> do
             pokeArray pst (replicate n 0)
-            rc <- c_decode (castPtr pin) poffs (fromIntegral n) ty pm pst
+            rc <- c_decode (castPtr pin) (fromIntegral (BS.length bytes)) poffs (fromIntegral n) ty pm pst
             if rc /= 0
               then pure (Left ("pxb_wire_decode_host failed: " <> show rc))
               else do

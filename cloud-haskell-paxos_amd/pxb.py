@@ -192,9 +192,10 @@ def load(path: str = LIB_PATH):
     for name, args in (("pxb_wire_size", [vp, C.c_uint64, C.c_uint32, vp, vp]),
                        ("pxb_wire_encode", [vp, C.c_uint64, C.c_uint32, vp, vp, vp]),
                        ("pxb_wire_encode_all", [vp, C.c_uint64, C.c_uint32, vp, vp, vp]),
-                       ("pxb_wire_decode", [vp, vp, C.c_uint64, C.c_uint32, vp, vp, vp]),
+                       ("pxb_wire_decode", [vp, C.c_uint64, vp, C.c_uint64, C.c_uint32, vp, vp, vp]),
                        ("pxb_wire_encode_host", [vp, C.c_uint64, C.c_uint32, vp, vp, vp]),
-                       ("pxb_wire_decode_host", [vp, vp, C.c_uint64, C.c_uint32, vp, vp])):
+                       ("pxb_wire_decode_host", [vp, C.c_uint64, vp, C.c_uint64, C.c_uint32, vp, vp]),
+                       ("pxb_init", [C.c_int]), ("pxb_shutdown", [])):
         getattr(lib, name).argtypes = args
         getattr(lib, name).restype = C.c_int
     _lib = lib
@@ -315,6 +316,28 @@ def wire_encode_device(d_msgs, wire_type, d_offsets, d_bytes, stream=None):
                                   C.c_void_p(d_bytes.data_ptr()), C.c_void_p(stream or 0)))
 
 
+def wire_decode_device(d_bytes, d_offsets, n, wire_type, d_msgs, d_status=None, stream=None):
+    """pxb_wire_decode on device tensors: d_bytes uint8 (its whole length is the
+    buffer bound), d_offsets int64 (n + 1), d_msgs int32 (n, 4), d_status int32
+    (n,) or None; asynchronous on `stream` (raw hipStream_t, default if None)."""
+    lib = load()
+    assert d_offsets.numel() >= n + 1 and d_msgs.shape[0] >= n
+    check(lib.pxb_wire_decode(C.c_void_p(d_bytes.data_ptr()), d_bytes.numel(), C.c_void_p(d_offsets.data_ptr()), n,
+                              wire_type, C.c_void_p(d_msgs.data_ptr()),
+                              C.c_void_p(d_status.data_ptr() if d_status is not None else 0), C.c_void_p(stream or 0)))
+
+
+def init(n_devices: int = 0):
+    """pxb_init: allocate the per-device scratch of devices 0..n-1 up front."""
+    check(load().pxb_init(n_devices))
+
+
+def shutdown():
+    """pxb_shutdown: free every per-device scratch buffer and the cached RCCL
+    communicators (the next call allocates them again)."""
+    check(load().pxb_shutdown())
+
+
 def wire_decode(data: bytes, offsets, wire_type):
     """Inverse of wire_encode: (msgs (n, 4) uint32, status (n,) uint32)."""
     import numpy as np
@@ -325,5 +348,5 @@ def wire_decode(data: bytes, offsets, wire_type):
     buf = np.ascontiguousarray(buf)
     msgs = np.zeros((max(n, 0), 4), dtype=np.uint32)
     st = np.zeros(max(n, 0), dtype=np.uint32)
-    check(lib.pxb_wire_decode_host(_ptr(buf), _ptr(offs), n, wire_type, _ptr(msgs), _ptr(st)))
+    check(lib.pxb_wire_decode_host(_ptr(buf), len(data), _ptr(offs), n, wire_type, _ptr(msgs), _ptr(st)))
     return msgs, st

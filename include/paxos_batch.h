@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PXB_ABI_VERSION 2
+#define PXB_ABI_VERSION 3   /* 3: pxb_init / pxb_shutdown, n_bytes bound on wire decode */
 
 /* ---- error codes ---------------------------------------------------------- */
 #define PXB_OK          0
@@ -134,12 +134,16 @@ int pxb_run(const pxb_config* cfg, pxb_result* out, uint32_t* log_digest,
 /* pxb_run_device: DEVICE buffers, asynchronous on `stream` (a hipStream_t;
  * NULL = default stream).  Same outputs as pxb_run but all pointers are device
  * pointers on the current device.  d_totals (PXB_NCOUNTERS int64) is ADDED to,
- * not overwritten, so many launches can accumulate into one vector.  Each
- * call enqueues the batch kernel and a one-block finalize kernel (it folds
- * the per-launch partial totals into d_totals) per chunk of the batch (2^29
- * instances at most on faulty schedules), each chunk using one of 64
- * per-device scratch slots round-robin: at most 64 chunks per device may be
- * in flight at once across streams.                                        */
+ * not overwritten, so many launches can accumulate into one vector.  The
+ * batch runs in chunks; each chunk enqueues its kernels (faulty single-decree
+ * batches: the per-lane kernel, then the general kernel over the instances it
+ * handed back) and a one-block finalize kernel that folds the chunk's partial
+ * totals into d_totals.  Chunks: at most 2^24 instances on the per-lane
+ * kernel, 2^30 - 1 on the general faulty kernel, 2^31 fault-free.  Each chunk
+ * uses one of 64 per-device scratch slots round-robin: at most 64 chunks per
+ * device may be in flight at once across streams.  A launch failure after a
+ * chunk's first kernel zeroes its slot (behind the queued work) before the
+ * error is returned.                                                         */
 int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_digest,
                    pxb_acceptor_rec* d_acc, int64_t* d_totals, void* stream);
 
@@ -150,6 +154,20 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
  * the global instance id).  Replaces: Main.hs:37-53 for a multi-GPU node.     */
 int pxb_run_multi(const pxb_config* cfg, int n_devices, pxb_result* out, uint32_t* log_digest,
                   pxb_acceptor_rec* acc, pxb_counters* totals);
+
+/* ---- context ------------------------------------------------------------------
+ * The library keeps per-device scratch (64 launch slots of partial totals and
+ * queue words, the per-lane kernel's bailed-id lists, the wire codec's scan
+ * buffer) and the RCCL communicators of pxb_run_multi, created lazily on
+ * first use.  pxb_init(n) creates the scratch of devices 0..n-1 (n <= 0: all
+ * visible) up front; pxb_shutdown() waits for those devices, frees everything
+ * and destroys the communicators; the next call starts afresh.  Both are
+ * optional.  Do not call pxb_shutdown while other threads have calls in
+ * flight.  (A CPU pxb_run_cpu is NOT part of this library: the CPU
+ * restatement of the schedule is test infrastructure in oracle/ — the checker
+ * and the timed baseline — and the GPU entry points never fall back to it.) */
+int pxb_init(int n_devices);
+int pxb_shutdown(void);
 
 /* ---- single-handler hooks (run the kernel's own device functions) -------- */
 /* One message in or out.  Requests (ClientRequest, Common.hs:41-45):
@@ -217,8 +235,9 @@ int pxb_proposer_handle(pxb_proposer_rec* states, uint32_t n_acceptors,
  * offsets of `count` encoded messages (d_offsets: count + 1 entries);
  * pxb_wire_encode takes exactly those offsets (it writes the records of each
  * message tile contiguously from the tile's first offset).  Decode
- * accepts any offsets within the buffer: a record with off[i+1] < off[i] is
- * empty (PXB_WIRE_E_LENGTH). */
+ * accepts any offsets: a record with off[i+1] < off[i] is empty, and one that
+ * reaches past n_bytes (the size of d_bytes) is never read; both are
+ * PXB_WIRE_E_LENGTH. */
 int pxb_wire_size(const pxb_msg* d_msgs, uint64_t count, uint32_t type, uint64_t* d_offsets, void* stream);
 int pxb_wire_encode(const pxb_msg* d_msgs, uint64_t count, uint32_t type, const uint64_t* d_offsets,
                     uint8_t* d_bytes, void* stream);
@@ -229,14 +248,14 @@ int pxb_wire_encode(const pxb_msg* d_msgs, uint64_t count, uint32_t type, const 
 int pxb_wire_encode_all(const pxb_msg* d_msgs, uint64_t count, uint32_t type, uint64_t* d_offsets,
                         uint8_t* d_bytes, void* stream);
 /* d_status (nullable): PXB_WIRE_* per message; failed messages decode to 0s */
-int pxb_wire_decode(const uint8_t* d_bytes, const uint64_t* d_offsets, uint64_t count, uint32_t type,
-                    pxb_msg* d_msgs, uint32_t* d_status, void* stream);
+int pxb_wire_decode(const uint8_t* d_bytes, uint64_t n_bytes, const uint64_t* d_offsets, uint64_t count,
+                    uint32_t type, pxb_msg* d_msgs, uint32_t* d_status, void* stream);
 /* HOST-buffer forms (blocking).  encode: `out` holds count * PXB_WIRE_MAX_BYTES
  * bytes, offsets count + 1 entries, *nbytes = total bytes written. */
 int pxb_wire_encode_host(const pxb_msg* msgs, uint64_t count, uint32_t type, uint8_t* out, uint64_t* offsets,
                          uint64_t* nbytes);
-int pxb_wire_decode_host(const uint8_t* in, const uint64_t* offsets, uint64_t count, uint32_t type,
-                         pxb_msg* msgs, uint32_t* status);
+int pxb_wire_decode_host(const uint8_t* in, uint64_t n_bytes, const uint64_t* offsets, uint64_t count,
+                         uint32_t type, pxb_msg* msgs, uint32_t* status);
 
 /* ---- misc ----------------------------------------------------------------- */
 const char* pxb_strerror(int code);

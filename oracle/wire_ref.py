@@ -170,6 +170,16 @@ def decode(b: bytes, kind: int) -> Tuple[int, Tuple[int, int, int, int]]:
         return e.code, (0, 0, 0, 0)
 
 
+def decode_at(buf: bytes, b: int, e: int, kind: int) -> Tuple[int, Tuple[int, int, int, int]]:
+    """Record i of a batch: bytes [b, max(b, e)) of the buffer.  A record that
+    reaches past the end of the buffer is a length error (the n_bytes bound
+    of pxb_wire_decode); the decode itself is `decode`."""
+    e = max(b, e)
+    if e > len(buf):
+        return E_LENGTH, (0, 0, 0, 0)
+    return decode(buf[b:e], kind)
+
+
 def encode_batch(msgs, kind: int) -> Tuple[bytes, List[int]]:
     out, offs = [], [0]
     for m in msgs:

@@ -22,7 +22,8 @@ def _declared():
 def test_header_declares_the_boundary():
     names = _declared()
     for f in ("pxb_run", "pxb_run_device", "pxb_acceptor_handle", "pxb_proposer_handle",
-              "pxb_strerror", "pxb_last_hip_error", "pxb_abi_version"):
+              "pxb_strerror", "pxb_last_hip_error", "pxb_abi_version", "pxb_init", "pxb_shutdown",
+              "pxb_run_multi"):
         assert f in names
 
 
@@ -59,7 +60,7 @@ int main(void) {
 
 def test_misc_entry_points_without_gpu():
     lib = pxb.load()
-    assert lib.pxb_abi_version() == 2
+    assert lib.pxb_abi_version() == 3
     assert lib.pxb_strerror(pxb.PXB_E_INVAL) == b"invalid argument"
     assert lib.pxb_canonical_bytes_nofault(5) == 1140
 
@@ -79,3 +80,24 @@ def test_no_cpu_fallback_without_gpu():
         pytest.skip("GPU present")
     with pytest.raises(pxb.PaxosError):
         pxb.run(pxb.CONFIGS[2], 0, 16)
+
+
+def test_init_and_shutdown_without_gpu():
+    """The context entry points fail cleanly without a device; shutdown with
+    nothing allocated is a no-op, and may be repeated."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    lib = pxb.load()
+    assert lib.pxb_init(0) == pxb.PXB_E_NODEV
+    assert lib.pxb_shutdown() == pxb.PXB_OK
+    assert lib.pxb_shutdown() == pxb.PXB_OK
+
+
+def test_multi_without_gpu_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    lib = pxb.load()
+    c = pxb.CONFIGS[3].to_c(0, 100)
+    assert lib.pxb_run_multi(C.byref(c), 0, None, None, None, None) == pxb.PXB_E_NODEV

@@ -335,6 +335,41 @@ def test_run_multi_matches_single_device(gpu_lib):
     assert np.array_equal(res, eres) and np.array_equal(dig, edig) and cnt == ecnt
 
 
+@pytest.mark.parametrize("phase", ["setup", "compute"])
+def test_run_multi_shard_failure_returns_promptly(gpu_lib, phase):
+    """A device that fails before the collective makes pxb_run_multi return its
+    error at once (no device is left blocked in the all-reduce); the next call
+    works."""
+    import time
+    cfg = pxb.CONFIGS[3]
+    os.environ["PXB_MULTI_FAIL_PHASE"], os.environ["PXB_MULTI_FAIL_DEVICE"] = phase, "0"
+    try:
+        t0 = time.perf_counter()
+        with pytest.raises(pxb.PaxosError):
+            pxb.run_multi(cfg, 0, 5000)
+        assert time.perf_counter() - t0 < 60
+    finally:
+        del os.environ["PXB_MULTI_FAIL_PHASE"], os.environ["PXB_MULTI_FAIL_DEVICE"]
+    res, _, cnt = pxb.run_multi(cfg, 0, 5000)
+    assert cnt["instances"] == 5000
+
+
+def test_init_shutdown_cycles(gpu_lib):
+    """pxb_init / pxb_shutdown release and rebuild every per-device buffer and
+    the cached communicators; runs in between stay exact."""
+    cfg = pxb.CONFIGS[4]
+    want = pxb.run(cfg, 0, 3000)
+    for _ in range(3):
+        pxb.init(0)
+        got = pxb.run(cfg, 0, 3000)
+        assert np.array_equal(got[0], want[0]) and got[3] == want[3]
+        pxb.run_multi(cfg, 0, 1000)
+        pxb.shutdown()
+    pxb.shutdown()
+    got = pxb.run(cfg, 0, 3000)
+    assert np.array_equal(got[0], want[0])
+
+
 def test_host_driver_binary(gpu_lib):
     """The C++ batch driver (the app/Main.hs role) runs config 1 end to end."""
     import subprocess

@@ -148,7 +148,8 @@ def test_gpu_decode_irregular_offsets_matches_oracle(gpu_lib, kind):
     """Offsets that are not a clean framing: decreasing pairs (an empty record),
     a tile whose range runs backwards, a tile whose range exceeds the LDS stage.
     Every record i is bytes[offs[i]:max(offs[i], offs[i+1])], as in the oracle;
-    such tiles are parsed from HBM instead of the LDS stage."""
+    such tiles are parsed from HBM instead of the LDS stage.  Offsets past the
+    end of the buffer make a length error and are never read."""
     rng = np.random.default_rng(21 + kind)
     msgs = _batch(kind, 5000, 17 + kind)
     data, offs = pxb.wire_encode(msgs, kind)
@@ -158,10 +159,13 @@ def test_gpu_decode_irregular_offsets_matches_oracle(gpu_lib, kind):
         offs[i] = int(rng.integers(0, total + 1))       # random framing errors
     offs[1024] = total                                   # tile 0 too long, tile 1 backwards
     offs[3000] = 0
+    for i in rng.choice(np.arange(1, 5000), 12, replace=False):
+        offs[i] = total + int(rng.integers(1, 1 << 20))  # past the end of the buffer
+    offs[-1] = total + 7
     got, st = pxb.wire_decode(data, offs, kind)
     for i in range(5000):
         b, e = int(offs[i]), int(offs[i + 1])
-        ws, wm = W.decode(data[b:max(b, e)], kind)
+        ws, wm = W.decode_at(data, b, e, kind)
         assert st[i] == ws, (i, b, e, st[i], ws)
         if ws == W.OK:
             assert _as_msg(got[i]) == wm
