@@ -54,6 +54,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true")
+    ap.add_argument("--dry-run", action="store_true", help="CPU ranks (gloo), synthetic work: launcher test only")
     return ap.parse_args()
 
 
@@ -81,91 +82,143 @@ def step_instances(c: int, override: int) -> int:
     return pxb.CONFIG_INSTANCES[c]
 
 
-def run_workload(cfg, n, steps, warmup, rank, world, stream, dev, warm_n=None):
-    """Times `steps` back-to-back pxb_run_device calls of n fresh instances.
+class GpuLeg:
+    """The measured work of one rank: pxb_run_device over fresh instance ids,
+    asynchronous on one HIP stream, timed with an event pair on that stream."""
+
+    def __init__(self, cfg, n, rank, world, stream, dev):
+        import torch
+        import pxb
+        self.torch, self.pxb = torch, pxb
+        self.cfg, self.n, self.rank, self.world, self.stream, self.dev = cfg, n, rank, world, stream, dev
+        self.out = torch.empty((n, 4), dtype=torch.int32, device=dev)
+        self.dig = torch.empty((n, cfg.n_acceptors), dtype=torch.int32, device=dev)
+        self.tot = torch.zeros(16, dtype=torch.int64, device=dev)
+        self.e0 = torch.cuda.Event(enable_timing=True)
+        self.e1 = torch.cuda.Event(enable_timing=True)
+
+    def launch(self, step, count):
+        first = (step * self.world + self.rank) * self.n      # fresh global instance ids per step/rank
+        with self.torch.cuda.stream(self.stream):
+            self.pxb.run_device(self.cfg, first, count, d_results=self.out, d_digests=self.dig, d_totals=self.tot,
+                                stream=self.stream.cuda_stream)
+
+    def sync(self):
+        self.torch.cuda.synchronize()
+
+    def mark(self, which):
+        # (e1 - e0) / K is the mean step time on the launch stream, gaps between kernels included
+        (self.e0 if which == 0 else self.e1).record(self.stream)
+
+    def event_ms(self):
+        return self.e0.elapsed_time(self.e1)
+
+
+class DryLeg:
+    """--dry-run: the same launcher, barriers, timing and collectives on CPU
+    ranks (gloo) with a synthetic stand-in for the work (no Paxos is run: the
+    'totals' are instance counts).  Lets tests/test_bench_launch.py exercise the
+    N-rank path of this file without GPUs."""
+
+    def __init__(self, n, rank, world):
+        import torch
+        self.torch, self.n = torch, n
+        self.tot = torch.zeros(16, dtype=torch.int64)
+        self.t = [0.0, 0.0]
+
+    def launch(self, step, count):
+        time.sleep(0.002)
+        self.tot[13] += count            # PXB_C_INSTANCES
+        self.tot[0] += count             # PXB_C_DECIDED
+
+    def sync(self):
+        pass
+
+    def mark(self, which):
+        self.t[which] = time.perf_counter()
+
+    def event_ms(self):
+        return (self.t[1] - self.t[0]) * 1e3
+
+
+def run_workload(leg, n, steps, warmup, world, warm_n=None):
+    """Times `steps` back-to-back launches of n fresh instances per rank.
     Returns (wall seconds for the timed steps, max over ranks; mean ms per step
-    from HIP events on the launch stream; run totals summed over ranks)."""
+    from the leg's events; run totals summed over ranks)."""
     import torch
     import torch.distributed as dist
-    import pxb
-    N = cfg.n_acceptors
-    out = torch.empty((n, 4), dtype=torch.int32, device=dev)
-    dig = torch.empty((n, N), dtype=torch.int32, device=dev)
-    tot = torch.zeros(16, dtype=torch.int64, device=dev)
-    sptr = stream.cuda_stream
-
-    def launch(step, count):
-        first = (step * world + rank) * n        # fresh global instance ids per step/rank
-        pxb.run_device(cfg, first, count, d_results=out, d_digests=dig, d_totals=tot, stream=sptr)
-
-    with torch.cuda.stream(stream):
-        for w in range(warmup):
-            launch(w, warm_n or n)
-        stream.synchronize()
-        tot.zero_()
-        # one event pair on the launch stream around the K back-to-back steps:
-        # (e1 - e0) / K is the mean step time, gaps between kernels included
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        e0.record(stream)
-        for k in range(steps):
-            launch(warmup + k, n)
-        e1.record(stream)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        t1 = time.perf_counter()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    for w in range(warmup):
+        leg.launch(w, warm_n or n)
+    leg.sync()
+    leg.tot.zero_()
+    if world > 1:
+        dist.barrier()
+    leg.sync()
+    t0 = time.perf_counter()
+    leg.mark(0)
+    for k in range(steps):
+        leg.launch(warmup + k, n)
+    leg.mark(1)
+    leg.sync()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=leg.tot.device)
     if world > 1:
         # after the timed region: the run totals (decided counts, violation
         # flags) summed over the node -- RCCL over xGMI, the only collective
-        dist.all_reduce(tot)
+        dist.all_reduce(leg.tot)
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    kms = e0.elapsed_time(e1) / steps
-    return float(elapsed.item()), kms, pxb.counters_dict(tot.cpu().tolist())
+    kms = leg.event_ms() / steps
+    return float(elapsed.item()), kms, counters_dict(leg.tot.cpu().tolist())
 
 
-def step_profile(workload: str, n: int):
-    """The committed rocprofv3 profile of this workload (tools/profile_round.sh
-    + tools/step_profile.py): PMC counts per step, or None."""
-    path = os.path.join(PROFILES, "r02_%s_step.json" % workload)
+def counters_dict(v):
+    import pxb                      # the names only (pxb.COUNTER_NAMES); loads no GPU code
+    return pxb.counters_dict(v)
+
+
+def step_profile(workload: str):
+    """The committed rocprofv3 profile of this workload (tools/profile_r02.sh
+    + tools/roofline.py): PMC counts per instance processed, or None."""
+    path = os.path.join(PROFILES, "r02_%s" % workload, "step.json")
     try:
         with open(path) as f:
-            p = json.load(f)
+            return json.load(f), path
     except (OSError, ValueError):
         return None, path
-    return (p if p.get("instances_per_step") == n else None), path
 
 
 def roofline(workload, n, kms, canon_bytes_per_step):
-    """VALU-issue roofline of one step: the PMC-counted VALU wave-instructions
-    of the step's kernels (committed profile of this workload) over the step
-    time measured now; HBM bytes from the same profile's FETCH/WRITE passes."""
-    prof, path = step_profile(workload, n)
-    canon_gbs = canon_bytes_per_step / (kms * 1e-3) / 1e9
+    """VALU-issue roofline of one step (per GPU): the PMC-counted VALU
+    wave-instructions per instance of this workload (committed profile of the
+    same command) x the step's instances, over the step time measured now with
+    HIP events on the launch stream; HBM bytes from the same profile's FETCH /
+    WRITE passes.  The canonical SURVEY.md 8(d) byte count is reported beside
+    it, never as frac: this engine does not move those bytes."""
+    prof, path = step_profile(workload)
+    step_s = kms * 1e-3
     r = {"bound": "valu_issue", "unit": "G VALU wave-instructions/s", "peak": VALU_PEAK_G,
          "achieved": None, "frac": None, "traffic": None,
          "peak_basis": "256 CUs x 2 wave64 VALU instructions per CU-cycle x 2.4 GHz (MI355X_MICROARCH.md)",
-         "canonical_equiv_GBps": canon_gbs,
+         "canonical_equiv_GBps": canon_bytes_per_step / step_s / 1e9,
          "canonical_note": "SURVEY.md 8(d) canonical bytes / step time: the traffic of a design whose "
                            "SoA state round-trips HBM every step; this engine keeps it on chip, so this "
                            "is not a bandwidth measurement",
          "physical_GBps": None, "physical_frac": None, "profile": os.path.relpath(path, ROOT)}
     if prof:
-        valu = prof["valu_insts_per_step"]
-        r["achieved"] = valu / (kms * 1e-3) / 1e9
+        valu = prof["valu_insts_per_instance"] * n
+        r["achieved"] = valu / step_s / 1e9
         r["frac"] = r["achieved"] / VALU_PEAK_G
         r["valu_insts_per_step"] = valu
-        r["dominant_kernel"] = prof.get("dominant_kernel")
-        r["dominant_share_of_step"] = prof.get("dominant_share")
-        hbm = prof.get("hbm_bytes_per_step")
-        if hbm is not None:
-            r["traffic"] = hbm
-            r["physical_GBps"] = hbm / (kms * 1e-3) / 1e9
-            r["physical_frac"] = r["physical_GBps"] / HBM_PEAK_GBS
+        r["valu_insts_per_instance"] = prof["valu_insts_per_instance"]
+        r["dominant_kernel"] = prof["dominant_kernel"]
+        r["dominant_share_of_kernel_time"] = prof["dominant_share"]
+        r["profile_kernel_ns_per_instance"] = prof["kernel_ns_per_instance"]
+        hbm = prof["hbm_bytes_per_instance"] * n
+        r["traffic"] = hbm
+        r["physical_GBps"] = hbm / step_s / 1e9
+        r["physical_frac"] = r["physical_GBps"] / HBM_PEAK_GBS
     return r
 
 
@@ -220,8 +273,11 @@ def wire_bench(stream, dev, n=1 << 24, reps=5):
 
 
 def host_cores():
-    """CPUs this process may run on, and the cgroup CPU quota if one is set."""
-    n = len(os.sched_getaffinity(0))
+    """(threads to use, CPUs in the process affinity, cgroup CPU quota or None).
+    The GPU box shows the whole machine in nproc / affinity but allots a 1-GPU
+    job its share (cgroup quota, and OMP_NUM_THREADS set to it): the baseline
+    runs one thread per CPU of that share, every CPU it may actually use."""
+    aff = len(os.sched_getaffinity(0))
     quota = None
     try:
         q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
@@ -229,7 +285,13 @@ def host_cores():
             quota = float(q) / float(per)
     except (OSError, ValueError):
         pass
-    return n, quota
+    n = aff
+    if quota:
+        n = min(n, max(1, int(quota)))
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return n, aff, quota
 
 
 def cpu_baseline(cfg, budget_s):
@@ -238,7 +300,7 @@ def cpu_baseline(cfg, budget_s):
     2^40), then on one core."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_c                          # CPU restatement (oracle/), baseline only
-    threads, quota = host_cores()
+    threads, aff, quota = host_cores()
     chunk = 1 << 17
     done, first = 0, 1 << 40
     t0 = time.perf_counter()
@@ -254,15 +316,16 @@ def cpu_baseline(cfg, budget_s):
         one += 1 << 14
     dt1 = time.perf_counter() - t1
     return {"value": done / dt, "unit": "instances/s", "cores": threads, "kind": "port",
-            "nproc": os.cpu_count(), "cgroup_cpu_quota": quota,
+            "nproc": os.cpu_count(), "affinity_cpus": aff, "cgroup_cpu_quota": quota,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
             "sample": "%d instances of the same config (ids from 2^40), oracle/paxos_oracle.c "
-                      "on %d host threads (all CPUs in the process affinity), %.1f s" % (done, threads, dt),
+                      "on %d host threads (every CPU of the job's share), %.1f s" % (done, threads, dt),
             "one_core": {"value": one / dt1, "sample": "%d further instances, 1 thread, %.1f s" % (one, dt1)}}
 
 
 def faulty_line(name, c, n, steps, warmup, stream, dev, warm_n):
     import pxb
-    es, ek, ecnt = run_workload(pxb.CONFIGS[c], n, steps, warmup, 0, 1, stream, dev, warm_n=warm_n)
+    es, ek, ecnt = run_workload(GpuLeg(pxb.CONFIGS[c], n, 0, 1, stream, dev), n, steps, warmup, 1, warm_n=warm_n)
     line = {"workload": name, "instances_per_step": n, "instances_per_s": ecnt["instances"] / es,
             "decided_per_s": ecnt["decided"] / es, "ms_per_step": es / steps * 1e3, "kernel_ms": ek,
             "mean_steps_per_instance": ecnt["steps"] / max(1, ecnt["instances"]),
@@ -270,6 +333,23 @@ def faulty_line(name, c, n, steps, warmup, stream, dev, warm_n):
     assert ecnt["instances"] == n * steps, ecnt
     assert ecnt["decided"] + ecnt["undecided"] == ecnt["instances"]
     return line
+
+
+def dry_main(args, rank, world):
+    """--dry-run: the N-rank launcher path on CPU (gloo); prints the JSON line
+    shape with a synthetic workload and "data": "dry-run" (not a measurement)."""
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+    n = args.instances or 1000
+    secs, kms, cnt = run_workload(DryLeg(n, rank, world), n, args.steps, args.warmup, world)
+    assert cnt["instances"] == n * world * args.steps, cnt
+    if rank == 0:
+        print(json.dumps({"metric": "dry-run", "value": cnt["decided"] / secs, "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": secs / args.steps * 1e3, "data": "dry-run",
+                          "rccl_world": world, "counters": cnt}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def main():
@@ -283,6 +363,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
+    if args.dry_run:
+        return dry_main(args, rank, world)
     import pxb
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -293,7 +375,7 @@ def main():
     cfg = pxb.CONFIGS[c]
     n = step_instances(c, args.instances)
 
-    secs, kms, cnt = run_workload(cfg, n, args.steps, args.warmup, rank, world, stream, dev)
+    secs, kms, cnt = run_workload(GpuLeg(cfg, n, rank, world, stream, dev), n, args.steps, args.warmup, world)
     total_inst = n * world * args.steps
     assert cnt["instances"] == total_inst, cnt
     if c == 2:   # closed forms of the fault-free config: every instance decides
@@ -337,7 +419,7 @@ def main():
         extra["wire_codec"] = wire_bench(stream, dev)
         # log mode: stock Main.hs topology with the ticker running (SEMANTICS §9)
         en = 1 << 20
-        es, ek, ecnt = run_workload(pxb.LOG_CONFIG, en, 2, 1, 0, 1, stream, dev)
+        es, ek, ecnt = run_workload(GpuLeg(pxb.LOG_CONFIG, en, 0, 1, stream, dev), en, 2, 1, 1)
         extra["log_mode"] = {"instances_per_step": en, "ticks_per_proposer": pxb.LOG_CONFIG.n_ticks,
                              "commands_committed_per_s": ecnt["executes"] / es,
                              "instances_per_s": ecnt["instances"] / es, "kernel_ms": ek, "counters": ecnt}

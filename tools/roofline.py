@@ -1,0 +1,94 @@
+"""Roofline figures of one bench workload from its rocprofv3 passes
+(tools/profile_r02.sh): kernel-trace stats, one SQ/GRBM PMC pass, FETCH_SIZE
+and WRITE_SIZE passes, all of the same `bench.py --no-cpu --no-extra` command.
+
+The engine keeps the protocol state on chip, so the bound is
+VALU issue, not HBM: a wave64 VALU instruction issues in 2 cycles on a SIMD-32
+(MI355X_MICROARCH.md, "Wave scheduling"), 4 SIMDs per CU, so the peak is
+2 wave-instructions per CU-cycle = 256 CUs x 2 x 2.4 GHz = 1,228.8 G/s.
+HBM bytes: FETCH_SIZE x 2 (gfx950 wide-read correction) + WRITE_SIZE, KiB.
+
+Everything is normalised per instance processed in the profiled run (warmup
++ timed steps), so bench.py can scale it to its own step and divide by the
+step time it measures live.
+    python tools/roofline.py <profile dir> <workload> <instances processed> [out.json]"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+CUS = 256
+PEAK_CLOCK_HZ = 2.4e9
+VALU_PER_CU_CYCLE = 2.0
+KERNEL_TAGS = ("paxos_ev_kernel", "paxos_batch_kernel", "finalize_kernel")
+
+
+def _tag(name):
+    for t in KERNEL_TAGS:
+        if t in name:
+            return t
+    return None
+
+
+def kernel_stats(root):
+    """{tag: (calls, total_ns)} from the kernel-trace stats CSV."""
+    out = defaultdict(lambda: [0, 0.0])
+    for f in glob.glob(os.path.join(root, "trace", "**", "*kernel_stats.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            t = _tag(r["Name"])
+            if t:
+                out[t][0] += int(r["Calls"])
+                out[t][1] += float(r["TotalDurationNs"])
+    return {k: tuple(v) for k, v in out.items()}
+
+
+def pmc_totals(root):
+    """{tag: {counter: sum over every dispatch}} from a --pmc pass."""
+    out = defaultdict(lambda: defaultdict(float))
+    for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            t = _tag(r.get("Kernel_Name", ""))
+            if t:
+                out[t][r["Counter_Name"]] += float(r["Counter_Value"])
+    return out
+
+
+def roofline(root, workload, instances):
+    ks = kernel_stats(root)
+    sq = pmc_totals(os.path.join(root, "valu"))
+    fe = pmc_totals(os.path.join(root, "fetch"))
+    wr = pmc_totals(os.path.join(root, "write"))
+    tot_ns = sum(v[1] for v in ks.values())
+    kern = {}
+    for t, (calls, ns) in sorted(ks.items()):
+        valu = sq[t].get("SQ_INSTS_VALU", 0.0)
+        grbm = sq[t].get("GRBM_GUI_ACTIVE", 0.0)
+        clock = min(grbm / 8.0 / (ns * 1e-9), PEAK_CLOCK_HZ) if ns and grbm else None
+        rate = valu / (ns * 1e-9) if ns else 0.0
+        kern[t] = {"calls": calls, "avg_us": ns / calls / 1e3 if calls else None, "share_of_time": ns / tot_ns,
+                   "valu_insts_per_instance": valu / instances,
+                   "salu_insts_per_instance": sq[t].get("SQ_INSTS_SALU", 0.0) / instances,
+                   "lds_insts_per_instance": sq[t].get("SQ_INSTS_LDS", 0.0) / instances,
+                   "achieved_G_valu_per_s": rate / 1e9,
+                   "effective_clock_MHz": clock / 1e6 if clock else None,
+                   "valu_frac_at_2400MHz": rate / (CUS * VALU_PER_CU_CYCLE * PEAK_CLOCK_HZ),
+                   "valu_frac_at_effective_clock": rate / (CUS * VALU_PER_CU_CYCLE * clock) if clock else None,
+                   "hbm_bytes_per_instance": (2.0 * fe[t].get("FETCH_SIZE", 0.0) + wr[t].get("WRITE_SIZE", 0.0))
+                   * 1024.0 / instances}
+    dom = max(kern, key=lambda t: kern[t]["share_of_time"])
+    return {"workload": workload, "instances_processed": instances,
+            "valu_insts_per_instance": sum(k["valu_insts_per_instance"] for k in kern.values()),
+            "hbm_bytes_per_instance": sum(k["hbm_bytes_per_instance"] for k in kern.values()),
+            "kernel_ns_per_instance": tot_ns / instances,
+            "dominant_kernel": dom, "dominant_share": kern[dom]["share_of_time"], "kernels": kern,
+            "peak_basis": "256 CUs x 2 wave64 VALU instructions per CU-cycle x 2.4 GHz = 1228.8 G/s "
+                          "(MI355X_MICROARCH.md); HBM = FETCH_SIZE x2 + WRITE_SIZE"}
+
+
+if __name__ == "__main__":
+    r = roofline(sys.argv[1], sys.argv[2], int(sys.argv[3]))
+    print(json.dumps(r, indent=1))
+    if len(sys.argv) > 4:
+        json.dump(r, open(sys.argv[4], "w"), indent=1)
