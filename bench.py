@@ -395,7 +395,7 @@ def main():
         "dtype": "int32",
         "data": "synthetic (Philox4x32-10 schedule from seed + global instance id)",
         "config": {"workload": "BASELINE config %d" % c + (
-                       ": %d batches of 2^20 instances per step" % (n >> 20) if c == 2 else ""),
+                       ": %d fresh instances per GPU per step (%d x the 2^20 batch)" % (n, n >> 20) if c == 2 else ""),
                    "instances_per_gpu_per_step": n,
                    "proposers": cfg.n_proposers, "acceptors": cfg.n_acceptors,
                    "loss_ppm": cfg.loss_ppm, "delay_max": cfg.delay_max, "skew_max": cfg.skew_max,

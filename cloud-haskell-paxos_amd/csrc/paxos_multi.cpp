@@ -93,7 +93,7 @@ struct HipShards {
     pxb_acceptor_rec* d_acc = nullptr;
     int64_t* d_tot = nullptr;
     uint64_t lo = 0, m = 0;
-    int64_t tot[PXB_NCOUNTERS];
+    int64_t tot[PXB_NCOUNTERS] = {0};
   };
   std::vector<Dev> dv;
 
@@ -162,7 +162,11 @@ struct HipShards {
     if (d.d_acc) (void)hipFree(d.d_acc);
     if (d.d_tot) (void)hipFree(d.d_tot);
     if (d.st) (void)hipStreamDestroy(d.st);
-    d = Dev();
+    d.st = nullptr;                  // (the fetched totals stay: they are the result)
+    d.d_out = nullptr;
+    d.d_dig = nullptr;
+    d.d_acc = nullptr;
+    d.d_tot = nullptr;
   }
 };
 
