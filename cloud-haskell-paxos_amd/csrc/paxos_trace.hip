@@ -1,0 +1,157 @@
+// paxos_trace.hip — pxb_trace_instance: one instance through the per-lane state
+// machine (paxos_ev.h) on one GPU lane, with its state recorded at the end of
+// every visited step: the device counterpart of the reference's per-message
+// `say` dumps (Server.hs:85, Client.hs:108), used to localise a parity break.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include "../../include/paxos_batch.h"
+#include "paxos_ev_kernel.h"
+
+namespace pxb {
+namespace ev {
+
+template <int PM, int N, int POOL, int W, class Mem>
+__device__ void trace_record(const EvLane<PM, N, POOL, W, false, Mem>& L, uint32_t step, pxb_trace_step* r) {
+  r->step = step;
+  r->in_flight = L.in_flight;
+  r->n_acceptors = N;
+  r->n_proposers = L.P;
+  for (int a = 0; a < PXB_MAX_ACCEPTORS; ++a) {
+    uint32_t rec[4] = {0, 0, 0, 0};
+    if (a < N) L.record_of(a, rec);
+    r->acc[a].t_max = (int32_t)rec[0];
+    r->acc[a].t_store = (int32_t)rec[1];
+    r->acc[a].val = rec[2];
+    r->acc[a].meta = rec[3];
+    r->log_digest[a] = a < N ? L.digest_of(a) : 0u;
+  }
+  for (int p = 0; p < PXB_MAX_PROPOSERS; ++p) {
+    pxb_trace_prop q = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (p < PM && (uint32_t)p < L.P) {
+      const uint32_t code = 1u;   // every command is c<id>.1 (docs/SEMANTICS.md §2)
+      q.ticket = (int32_t)L.ticket[p];
+      q.cmd = L.cmd[p] ? ((L.cmd[p] << 24) | code) : 0u;
+      q.acks = L.acks[p];
+      q.state = L.rs[p];
+      q.mr_t = (int32_t)L.mr_t[p];
+      q.mr_v = L.mr_v[p] ? ((L.mr_v[p] << 24) | code) : 0u;
+      q.r2_v = L.r2_v[p] ? ((L.r2_v[p] << 24) | code) : 0u;
+      q.pending = L.pending[p];
+    }
+    r->prop[p] = q;
+  }
+}
+
+// one wave, lane 0 runs the instance; status[0] = records written,
+// status[1] = 1 bailed / 2 out of records
+template <int PM, int N, int W>
+__global__ __launch_bounds__(64) void paxos_trace_kernel(EvParams p, uint32_t gid, pxb_trace_step* out, uint32_t max,
+                                                         uint32_t* status, uint4* res) {
+  constexpr int POOL = EvPool<PM, N, false>::value;
+  using S = Shape<PM, N, POOL, W, false>;
+  __shared__ uint32_t lds[S::WORDS * 64];
+  if (threadIdx.x != 0) return;
+  EvLane<PM, N, POOL, W, false, LdsMem> L;
+  L.m = LdsMem{lds, 0u};
+  L.init(p, gid);
+  uint32_t n = 0;
+  for (;;) {
+    const int32_t s0 = L.s;
+    EvOut o;
+    const bool done = L.step(p, o);
+    if (L.bailed) {
+      status[1] = 1u;
+      break;
+    }
+    if (done || L.s != s0) {
+      if (n >= max) {
+        status[1] = 2u;
+        break;
+      }
+      trace_record(L, (uint32_t)(done ? L.s : s0), out + n);
+      ++n;
+    }
+    if (done) {
+      *res = make_uint4(o.res[0], o.res[1], o.res[2], o.res[3]);
+      break;
+    }
+  }
+  status[0] = n;
+}
+
+typedef void (*trace_ptr)(EvParams, uint32_t, pxb_trace_step*, uint32_t, uint32_t*, uint4*);
+
+template <int PM, int W>
+static trace_ptr pick_n(uint32_t n) {
+  switch (n) {
+    case 2: return paxos_trace_kernel<PM, 2, W>;
+    case 3: return paxos_trace_kernel<PM, 3, W>;
+    case 4: return paxos_trace_kernel<PM, 4, W>;
+    case 5: return paxos_trace_kernel<PM, 5, W>;
+    case 6: return paxos_trace_kernel<PM, 6, W>;
+    case 7: return paxos_trace_kernel<PM, 7, W>;
+    case 8: return paxos_trace_kernel<PM, 8, W>;
+    case 9: return paxos_trace_kernel<PM, 9, W>;
+  }
+  return nullptr;
+}
+
+static trace_ptr pick(uint32_t pm, uint32_t n, int w) {
+  switch (pm * 100 + (uint32_t)w) {
+    case 108: return pick_n<1, 8>(n);
+    case 116: return pick_n<1, 16>(n);
+    case 208: return pick_n<2, 8>(n);
+    case 216: return pick_n<2, 16>(n);
+    case 308: return pick_n<3, 8>(n);
+    case 316: return pick_n<3, 16>(n);
+  }
+  return nullptr;
+}
+
+}  // namespace ev
+}  // namespace pxb
+
+extern "C" int pxb_trace_instance(const pxb_config* cfg, uint64_t instance, pxb_trace_step* out, uint32_t max_records,
+                                  uint32_t* n_records, pxb_result* result) {
+  using namespace pxb::ev;
+  if (!cfg || !out || !n_records || max_records == 0) return PXB_E_INVAL;
+  if (cfg->n_proposers < 1 || cfg->n_proposers > PXB_MAX_PROPOSERS || cfg->n_acceptors < PXB_MIN_ACCEPTORS ||
+      cfg->n_acceptors > PXB_MAX_ACCEPTORS || cfg->delay_max < 1 || cfg->delay_max > PXB_MAX_DELAY ||
+      cfg->step_cap < 1 || !eligible(cfg))
+    return PXB_E_INVAL;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return PXB_E_NODEV;
+  const trace_ptr fn = pick(cfg->n_proposers, cfg->n_acceptors, wheel_for(cfg->delay_max));
+  if (!fn) return PXB_E_INVAL;
+  EvParams p = make_params(cfg);
+  p.first_instance = instance;
+  pxb_trace_step* d_out = nullptr;
+  uint32_t* d_st = nullptr;
+  uint4* d_res = nullptr;
+  int rc = PXB_OK;
+  hipError_t e = hipSuccess;
+  uint32_t st[2] = {0, 0};
+  do {
+    if ((e = hipMalloc(&d_out, (size_t)max_records * sizeof(pxb_trace_step))) != hipSuccess) break;
+    if ((e = hipMalloc(&d_st, 2 * sizeof(uint32_t))) != hipSuccess) break;
+    if ((e = hipMalloc(&d_res, sizeof(uint4))) != hipSuccess) break;
+    if ((e = hipMemset(d_st, 0, 2 * sizeof(uint32_t))) != hipSuccess) break;
+    hipLaunchKernelGGL(fn, dim3(1), dim3(64), 0, 0, p, 0u, d_out, max_records, d_st, d_res);
+    if ((e = hipGetLastError()) != hipSuccess) break;
+    if ((e = hipDeviceSynchronize()) != hipSuccess) break;
+    if ((e = hipMemcpy(st, d_st, sizeof(st), hipMemcpyDeviceToHost)) != hipSuccess) break;
+    if (st[1]) {
+      rc = PXB_E_INVAL;
+      break;
+    }
+    if ((e = hipMemcpy(out, d_out, (size_t)st[0] * sizeof(pxb_trace_step), hipMemcpyDeviceToHost)) != hipSuccess) break;
+    if (result && (e = hipMemcpy(result, d_res, sizeof(uint4), hipMemcpyDeviceToHost)) != hipSuccess) break;
+    *n_records = st[0];
+  } while (0);
+  if (d_out) (void)hipFree(d_out);
+  if (d_st) (void)hipFree(d_st);
+  if (d_res) (void)hipFree(d_res);
+  if (e != hipSuccess) return (e == hipErrorOutOfMemory) ? PXB_E_OOM : PXB_E_HIP;
+  return rc;
+}

@@ -195,7 +195,8 @@ def load(path: str = LIB_PATH):
                        ("pxb_wire_decode", [vp, C.c_uint64, vp, C.c_uint64, C.c_uint32, vp, vp, vp]),
                        ("pxb_wire_encode_host", [vp, C.c_uint64, C.c_uint32, vp, vp, vp]),
                        ("pxb_wire_decode_host", [vp, C.c_uint64, vp, C.c_uint64, C.c_uint32, vp, vp]),
-                       ("pxb_init", [C.c_int]), ("pxb_shutdown", [])):
+                       ("pxb_init", [C.c_int]), ("pxb_shutdown", []),
+                       ("pxb_trace_instance", [vp, C.c_uint64, vp, C.c_uint32, vp, vp])):
         getattr(lib, name).argtypes = args
         getattr(lib, name).restype = C.c_int
     _lib = lib
@@ -325,6 +326,30 @@ def wire_decode_device(d_bytes, d_offsets, n, wire_type, d_msgs, d_status=None, 
     check(lib.pxb_wire_decode(C.c_void_p(d_bytes.data_ptr()), d_bytes.numel(), C.c_void_p(d_offsets.data_ptr()), n,
                               wire_type, C.c_void_p(d_msgs.data_ptr()),
                               C.c_void_p(d_status.data_ptr() if d_status is not None else 0), C.c_void_p(stream or 0)))
+
+
+TRACE_WORDS = 4 + 9 * 4 + 9 + 3 * 8      # pxb_trace_step, uint32 words
+
+
+def trace_instance(cfg: Config, instance: int, max_records: int = 8192):
+    """pxb_trace_instance: the state at the end of every visited step of one
+    instance, as a list of dicts (step, in_flight, acc (N, 4), digest (N,),
+    prop (P, 8): ticket, cmd, acks, state, mr_t, mr_v, r2_v, pending), and its
+    pxb_result."""
+    import numpy as np
+    lib = load()
+    buf = np.zeros((max_records, TRACE_WORDS), dtype=np.uint32)
+    nrec = C.c_uint32(0)
+    res = np.zeros(4, dtype=np.uint32)
+    c = cfg.to_c(instance, 1)
+    check(lib.pxb_trace_instance(C.byref(c), instance, _ptr(buf), max_records, C.byref(nrec), _ptr(res)))
+    out = []
+    for r in buf[:nrec.value]:
+        N, P = int(r[2]), int(r[3])
+        out.append({"step": int(r[0]), "in_flight": int(r[1]),
+                    "acc": r[4:4 + 36].reshape(9, 4)[:N].copy(), "digest": r[40:49][:N].copy(),
+                    "prop": r[49:49 + 24].reshape(3, 8)[:P].copy()})
+    return out, res
 
 
 def init(n_devices: int = 0):

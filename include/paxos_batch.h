@@ -169,6 +169,39 @@ int pxb_run_multi(const pxb_config* cfg, int n_devices, pxb_result* out, uint32_
 int pxb_init(int n_devices);
 int pxb_shutdown(void);
 
+/* ---- per-instance trace (the build counterpart of the reference's `say`
+ * state dumps, Server.hs:85 and Client.hs:108) ---------------------------------
+ * Runs ONE instance of a single-decree batch on the current device through the
+ * per-lane state machine of the faulty kernels (csrc/paxos_ev.h) and records
+ * the state at the end of every step it visits: steps with no due message and
+ * no Tick change nothing and are skipped (their state is the previous
+ * record's).  Host buffers; out holds max_records records; *n_records is the
+ * count written (the last one is the final step); result (nullable) is the
+ * instance's pxb_result, as pxb_run gives it.  PXB_E_INVAL for log mode, for
+ * step_cap > 4095, or if the instance outgrows the state machine's link
+ * capacities (its FIFOs hold 4 messages; the batch kernels then hand it to
+ * the general kernel) or max_records.                                        */
+typedef struct pxb_trace_prop {
+  int32_t  ticket;           /* _ticket                      Client.hs:60    */
+  uint32_t cmd;              /* _mCommand, (id << 24) | 1 or 0               */
+  uint32_t acks;             /* _numAcks                                     */
+  uint32_t state;            /* 0 Idle, 1 Round1, 2 Round2                    */
+  int32_t  mr_t;             /* Round1: MostRecent (ticket, command)          */
+  uint32_t mr_v;
+  uint32_t r2_v;             /* Round2: the proposed command                  */
+  uint32_t pending;          /* Round2: _originalCommandPending               */
+} pxb_trace_prop;
+typedef struct pxb_trace_step {
+  uint32_t step;             /* the step that just ended                      */
+  uint32_t in_flight;        /* messages queued on the links after it         */
+  uint32_t n_acceptors, n_proposers;
+  pxb_acceptor_rec acc[PXB_MAX_ACCEPTORS];
+  uint32_t log_digest[PXB_MAX_ACCEPTORS];
+  pxb_trace_prop prop[PXB_MAX_PROPOSERS];
+} pxb_trace_step;
+int pxb_trace_instance(const pxb_config* cfg, uint64_t instance, pxb_trace_step* out, uint32_t max_records,
+                       uint32_t* n_records, pxb_result* result);
+
 /* ---- single-handler hooks (run the kernel's own device functions) -------- */
 /* One message in or out.  Requests (ClientRequest, Common.hs:41-45):
  *   kind 0 AskForTicket t | 1 Propose (t, c) | 2 Execute t ; x = t, z = c.

@@ -454,8 +454,11 @@ class _Link:
 
 
 def run_instance(cfg: Config, inst: int, queue_depth: int = QUEUE_DEPTH,
-                 log_track: int = LOG_TRACK, ticket_limit: int = TICKET_LIMIT) -> InstanceResult:
-    """Run one instance under the canonical step schedule (docs/SEMANTICS.md)."""
+                 log_track: int = LOG_TRACK, ticket_limit: int = TICKET_LIMIT, trace=None) -> InstanceResult:
+    """Run one instance under the canonical step schedule (docs/SEMANTICS.md).
+    ``trace(s, accs, props, in_flight)``, if given, is called at the end of
+    every step with the live state (the reference's per-message `say` dumps,
+    Server.hs:85 / Client.hs:108, at step granularity)."""
     N = cfg.n_acceptors
     prm = instance_params(cfg, inst)
     P = prm.P
@@ -563,6 +566,9 @@ def run_instance(cfg: Config, inst: int, queue_depth: int = QUEUE_DEPTH,
                 flags |= F_TICKET_OVERFLOW
         # -- quiescence
         in_flight = any(l.q for row in req for l in row) or any(l.q for row in rsp for l in row)
+        if trace is not None:
+            trace(s, accs, props, sum(len(l.q) for row in req for l in row) +
+                  sum(len(l.q) for row in rsp for l in row))
         if not in_flight and s >= last_tick:
             break
     else:

@@ -406,3 +406,58 @@ def test_random_schedules_match_oracle(gpu_lib, i):
     rng = np.random.default_rng(0xF022 + i)
     cfg = _random_config(rng, i)
     _cmp(cfg, int(rng.integers(0, 1 << 34)), int(rng.integers(1, 1500)))
+
+
+# ---- per-instance trace (pxb_trace_instance; Server.hs:85 / Client.hs:108) ----
+def _oracle_trace(cfg, inst):
+    import paxos_ref as R
+    recs = []
+
+    def snap(s, accs, props, in_flight):
+        recs.append({"step": s, "in_flight": in_flight,
+                     "acc": [(a.t_max, a.t_store, a.val, len(a.log) | (int(a.dead) << 31)) for a in accs],
+                     "digest": [_digest(a.log) for a in accs],
+                     "prop": [(p.ticket, p.cmd, p.acks, p.rs, p.mr_t, p.mr_v, p.r2_v, int(p.pending))
+                              for p in props]})
+    res = R.run_instance(R.Config(**cfg.__dict__) if not isinstance(cfg, R.Config) else cfg, inst, trace=snap)
+    return recs, res
+
+
+def _digest(log):
+    import paxos_ref as R
+    h = R.FNV_BASIS
+    for v in log:
+        h = R.fnv1a_u32(h, v)
+    return R.fnv1a_u32(h, len(log))
+
+
+def _as_rec(g):
+    return {"step": g["step"], "in_flight": g["in_flight"],
+            "acc": [tuple(int(x) for x in r) for r in g["acc"]], "digest": [int(x) for x in g["digest"]],
+            "prop": [tuple(int(x) for x in r) for r in g["prop"]]}
+
+
+@pytest.mark.parametrize("c,inst", [(3, 0), (3, 17), (4, 5), (4, 123456), (5, 9), (5, 1000)])
+def test_trace_matches_oracle_steps(gpu_lib, c, inst):
+    """Every step the GPU trace records equals the oracle's state at the end of
+    that step (acceptor records, log digests, proposer states, messages in
+    flight); the steps it skips change nothing in the oracle either."""
+    cfg = pxb.CONFIGS[c]
+    try:
+        g, gres = pxb.trace_instance(cfg, inst)
+    except pxb.PaxosError:
+        pytest.skip("instance beyond the trace kernel's link capacities")
+    want, res = _oracle_trace(cfg, inst)
+    by_step = {r["step"]: r for r in want}
+    prev = None
+    gi = iter(_as_rec(x) for x in g)
+    cur = next(gi)
+    for r in want:
+        if cur is not None and r["step"] == cur["step"]:
+            assert r == cur, "step %d: oracle %s gpu %s" % (r["step"], r, cur)
+            prev, cur = cur, next(gi, None)
+        else:                                          # a skipped step: nothing changed
+            assert prev is not None and {k: r[k] for k in ("acc", "digest", "prop", "in_flight")} == \
+                {k: prev[k] for k in ("acc", "digest", "prop", "in_flight")}, r["step"]
+    assert cur is None and g[-1]["step"] == want[-1]["step"] and by_step
+    assert list(gres) == [res.decided_val, res.decided_ticket, res.rounds, res.packed_flags()]

@@ -271,3 +271,17 @@ def test_ticket_at_the_limit_sets_the_flag():
         top = max(p.ticket for p in R.run_instance(cfg, inst).proposers)
         assert R.run_instance(cfg, inst, ticket_limit=top).flags & R.F_TICKET_OVERFLOW
         assert not R.run_instance(cfg, inst, ticket_limit=top + 1).flags & R.F_TICKET_OVERFLOW
+
+
+def test_trace_callback_ends_at_the_final_state():
+    """run_instance's per-step trace (the oracle side of pxb_trace_instance):
+    one call per step, and the last snapshot is the final state."""
+    cfg = R.Config(seed=5, n_proposers=2, n_acceptors=5, loss_ppm=100000, delay_max=4, skew_max=3, step_cap=200)
+    for inst in range(20):
+        seen = []
+        res = R.run_instance(cfg, inst, trace=lambda s, a, p, f: seen.append(
+            (s, [(x.t_max, x.t_store, x.val, tuple(x.log)) for x in a], [(y.ticket, y.rs) for y in p], f)))
+        assert [x[0] for x in seen] == list(range(res.steps))
+        assert seen[-1][1] == [(x.t_max, x.t_store, x.val, tuple(x.log)) for x in res.acceptors]
+        assert seen[-1][2] == [(y.ticket, y.rs) for y in res.proposers]
+        assert (seen[-1][3] == 0) or (res.flags & R.F_STEP_CAP)
