@@ -2,11 +2,13 @@
 (tools/profile_round.sh, valu/) and the kernel-trace average duration.
 
 The batch kernel keeps the protocol state on chip, so its real limiter is
-VALU issue, not HBM.  Nominally a wave64 VALU instruction occupies its SIMD's
-16 lanes for 4 cycles (one wave-instruction per CU-cycle); the measured
-ceiling for simple 32-bit ops is higher (profiles/r01_valu_peak.jsonl).  The clock is the in-kernel effective clock,
-GRBM_GUI_ACTIVE / 8 XCDs / kernel time (MI355X_MICROARCH.md, DVFS give-back),
-capped at 2.4 GHz.
+VALU issue, not HBM.  A wave64 VALU instruction issues in 2 cycles on a
+SIMD-32, 4 SIMDs per CU: the peak is 2 wave-instructions per CU-cycle
+(MI355X_MICROARCH.md, "Wave scheduling").  (Round 1 used 1 per CU-cycle, half
+the peak, and reported fractions above 1; corrected in round 2.)  The clock is
+the in-kernel effective clock, GRBM_GUI_ACTIVE / 8 XCDs / kernel time
+(MI355X_MICROARCH.md, DVFS give-back), capped at 2.4 GHz.  tools/roofline.py
+is the round-2 tool (whole bench workloads, HBM passes included).
     python tools/valu_roofline.py <prof dir> <instances per launch> [out.json]"""
 import csv
 import glob
@@ -36,7 +38,7 @@ def roofline(root, instances):
     # the MI355X peak engine clock (2.4 GHz)
     clock_hz = min(s["GRBM_GUI_ACTIVE"] / 8.0 / (ns * 1e-9), 2.4e9)
     rate = s["SQ_INSTS_VALU"] / (ns * 1e-9)               # wave-instructions / s
-    peak = CUS * clock_hz
+    peak = CUS * 2.0 * clock_hz                           # 2 wave64 VALU instructions per CU-cycle
     # measured ceiling: tools/micro/valu_peak.hip (independent add/xor chains,
     # 8 waves/SIMD) issues ~1.4 wave-instructions per CU-cycle on gfx950
     emp = None
@@ -49,13 +51,11 @@ def roofline(root, instances):
             "lds_insts_per_instance": s["SQ_INSTS_LDS"] / instances,
             "salu_insts_per_instance": s["SQ_INSTS_SALU"] / instances,
             "achieved_G_wave_insts_per_s": rate / 1e9, "peak_G_wave_insts_per_s": peak / 1e9,
-            "frac_of_1_per_CU_cycle": rate / peak,
-            "measured_ceiling_G_wave_insts_per_s": None if emp is None else emp / 1e9,
-            "valu_issue_frac": None if emp is None else rate / emp,
-            "note": "1 wave64 VALU instruction per CU-cycle (4 SIMDs x 16 lanes, 4 cycles each) is the nominal "
-                    "rate; gfx950 issues simple 32-bit ops faster (tools/micro/valu_peak.hip: 1.4 per CU-cycle "
-                    "for add/xor chains, 0.98 for select chains), so valu_issue_frac is against that measured "
-                    "add/xor ceiling; PMC means per dispatch"}
+            "valu_frac": rate / peak,
+            "microbench_G_wave_insts_per_s": None if emp is None else emp / 1e9,
+            "note": "peak = 2 wave64 VALU instructions per CU-cycle (SIMD-32, 2 cycles per wave64 "
+                    "instruction, 4 SIMDs); the dependent-chain microbenchmark (tools/micro/valu_peak.hip, "
+                    "1.43 per CU-cycle) is not a ceiling; PMC means per dispatch"}
 
 
 if __name__ == "__main__":
