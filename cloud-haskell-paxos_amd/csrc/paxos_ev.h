@@ -206,17 +206,50 @@ struct EvLane {
 #endif
     return k;
   }
+  // Selects by a per-lane index q over a small register array, as bit
+  // operations on the one-hot word 1 << q: element i's lane mask is bit i of
+  // it sign-extended (one v_bfe_i32), merged with v_bfi_b32.  A compare per
+  // element would hold one 64-bit SGPR mask each, live across the step: for
+  // the N-acceptor arrays that pushed ~70 SGPRs into VGPR spill slots.
+  // (in asm: LLVM folds the bit form back into compares + v_cndmask)
+  template <int I>
+  __host__ __device__ static __forceinline__ uint32_t lane_mask(uint32_t onehot) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t r;
+    __asm__("v_bfe_i32 %0, %1, %2, 1" : "=v"(r) : "v"(onehot), "i"(I));
+    return r;
+#else
+    return (uint32_t)(((int32_t)(onehot << (31 - I))) >> 31);
+#endif
+  }
+  __host__ __device__ static __forceinline__ uint32_t bfi(uint32_t mk, uint32_t x, uint32_t y) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t r;
+    __asm__("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(mk), "v"(x), "v"(y));
+    return r;
+#else
+    return (mk & x) | (~mk & y);
+#endif
+  }
+  template <int K, int I = 1>
+  __host__ __device__ static __forceinline__ uint32_t get_from(const uint32_t (&v)[K], uint32_t oh, uint32_t r) {
+    if constexpr (I < K) return get_from<K, I + 1>(v, oh, bfi(lane_mask<I>(oh), v[I], r));
+    else return r;
+  }
   template <int K>
   __host__ __device__ static __forceinline__ uint32_t get(const uint32_t (&v)[K], uint32_t q) {
-    uint32_t r = opaque(v[0]);
-#pragma unroll
-    for (int i = 1; i < K; ++i) r = (q == (uint32_t)i) ? opaque(v[i]) : r;
-    return r;
+    return get_from<K>(v, 1u << q, v[0]);
+  }
+  template <int K, int I = 0>
+  __host__ __device__ static __forceinline__ void set_from(uint32_t (&v)[K], uint32_t oh, uint32_t x) {
+    if constexpr (I < K) {
+      v[I] = bfi(lane_mask<I>(oh), x, v[I]);
+      set_from<K, I + 1>(v, oh, x);
+    }
   }
   template <int K>
   __host__ __device__ static __forceinline__ void set(uint32_t (&v)[K], uint32_t q, uint32_t x, bool pred) {
-#pragma unroll
-    for (int i = 0; i < K; ++i) v[i] = (pred && q == (uint32_t)i) ? x : v[i];
+    set_from<K>(v, pred ? (1u << q) : 0u, x);
   }
 
   __host__ __device__ __forceinline__ uint32_t rsp_ld(uint32_t Lr) const { return m.ld(S::RSP + Lr); }
