@@ -144,6 +144,9 @@ struct EvOut {
 #ifndef PXB_EV_CPOST
 #define PXB_EV_CPOST 1
 #endif
+#ifndef PXB_EV_ACCN
+#define PXB_EV_ACCN 1       // acceptor ops per iteration
+#endif
 
 template <int PM, int N, int POOL, int W, bool CMP, class Mem>
 struct EvLane {
@@ -409,13 +412,11 @@ struct EvLane {
         set(nsent, cp, ck + 1u, true);
       }
     }
-    uint32_t d = 1u;
-    bool ok = true;
-    if (kp.cfg & EV_CFG_DRAWS) {                      // wave-uniform
-      const uint4 w = philox(lo, hi, ck, (1u << 24) | (cp << 8) | ca, skey(kp.k0), skey(kp.k1));
-      ok = !(lossy && w.x <= loss_m1);
-      d = faulty ? 1u + mulhi_n(w.y, dmax) : 1u;
-    }
+    // the draw is computed unconditionally (a branch around it would keep
+    // the iteration's three independent Philox chains from interleaving)
+    const uint4 w = philox(lo, hi, ck, (1u << 24) | (cp << 8) | ca, skey(kp.k0), skey(kp.k1));
+    const bool ok = !(lossy && w.x <= loss_m1);
+    const uint32_t d = faulty ? 1u + mulhi_n(w.y, dmax) : 1u;
     msgs += snd ? 1u : 0u;
     // enqueue (predicated: inactive lanes store to the dummy word)
     const bool go = snd && ok;
@@ -436,7 +437,8 @@ struct EvLane {
 
   // one iteration of all four parts; returns true when the instance ended (outputs in o)
   __host__ __device__ __forceinline__ bool step(const EvParams& kp, EvOut& o) {
-    acc_op(kp, true);
+#pragma unroll
+    for (int c = 0; c < PXB_EV_ACCN; ++c) acc_op(kp, true);
 #pragma unroll
     for (int c = 0; c < PXB_EV_CPRE; ++c) copy_send(kp, true);
     prop_op(kp, true);
@@ -504,13 +506,9 @@ struct EvLane {
     // Philox seq = the link's reply count.  Sent before the proposer part so its
     // state dies early; the proposer part only pops due-now heads, so the order
     // of the two on one link does not matter.
-    uint32_t d1 = 1u;
-    bool ok1 = true;
-    if (kp.cfg & EV_CFG_DRAWS) {                      // wave-uniform
-      const uint4 w1 = philox(lo, hi, kr, (1u << 24) | (1u << 16) | (p << 8) | a, skey(kp.k0), skey(kp.k1));
-      ok1 = !(lossy && w1.x <= loss_m1);
-      d1 = faulty ? 1u + mulhi_n(w1.y, dmax) : 1u;
-    }
+    const uint4 w1 = philox(lo, hi, kr, (1u << 24) | (1u << 16) | (p << 8) | a, skey(kp.k0), skey(kp.k1));
+    const bool ok1 = !(lossy && w1.x <= loss_m1);
+    const uint32_t d1 = faulty ? 1u + mulhi_n(w1.y, dmax) : 1u;
     msgs += snd1 ? 1u : 0u;
     bailed = bailed || (snd1 && kr == (S::CMP ? (1u << S::KB) - 1u : 0xFFFFu));
     if (!S::CMP) m.st16(snd1 ? S::RSEQ : S::DUMMY, snd1 ? L : 0u, kr + 1u);
