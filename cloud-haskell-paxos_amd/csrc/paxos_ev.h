@@ -169,8 +169,12 @@ struct EvLane {
   uint32_t in_mask;                   // this step's proposer inputs left (Tick / response links)
   uint32_t occ;                       // wheel slots holding due bits
   uint32_t iso;                       // acceptors isolated at step s
-  // proposer states (ClientState, Client.hs:58-67): tickets < 2^12, commands = clientId
-  uint32_t ticket[PM], cmd[PM], acks[PM], rs[PM], mr_t[PM], mr_v[PM], r2_v[PM], pending[PM];
+  uint32_t iso_next;                  // the next step at which iso changes
+  // proposer states (ClientState, Client.hs:58-67), packed (tickets < 2^12,
+  // commands = clientId, acks <= N/2 + 1):
+  //   pw0 = ticket [11:0] | mr_t [23:12] | acks [27:24] | state [29:28] | pending [30]
+  //   pw1 = mr_v [1:0] | r2_v [3:2] | cmd [5:4]
+  uint32_t pw0[PM], pw1[PM];
   uint32_t skew[PM];
   uint32_t nsent[PM];                 // broadcasts of p whose copies have started (request-link seq)
   uint32_t bnext[PM];                 // next broadcast-ring slot
@@ -255,17 +259,31 @@ struct EvLane {
     set_from<K>(v, pred ? (1u << q) : 0u, x);
   }
 
+  // fields of the packed proposer state of p (finish, trace)
+  __host__ __device__ uint32_t p_ticket(int p) const { return pw0[p] & 0xFFFu; }
+  __host__ __device__ uint32_t p_mr_t(int p) const { return (pw0[p] >> 12) & 0xFFFu; }
+  __host__ __device__ uint32_t p_acks(int p) const { return (pw0[p] >> 24) & 15u; }
+  __host__ __device__ uint32_t p_state(int p) const { return (pw0[p] >> 28) & 3u; }
+  __host__ __device__ uint32_t p_pending(int p) const { return (pw0[p] >> 30) & 1u; }
+  __host__ __device__ uint32_t p_mr_v(int p) const { return pw1[p] & 3u; }
+  __host__ __device__ uint32_t p_r2_v(int p) const { return (pw1[p] >> 2) & 3u; }
+  __host__ __device__ uint32_t p_cmd(int p) const { return (pw1[p] >> 4) & 3u; }
+
   __host__ __device__ __forceinline__ uint32_t rsp_ld(uint32_t Lr) const { return m.ld(S::RSP + Lr); }
   __host__ __device__ __forceinline__ void rsp_st(uint32_t Lr, uint32_t v) const { m.st(S::RSP + Lr, v); }
 
-  __host__ __device__ __forceinline__ uint32_t iso_at(int32_t t) const {
-    uint32_t r = 0u;
+  // the isolated acceptors at step t, and the next step at which that set changes
+  __host__ __device__ __forceinline__ void iso_update(int32_t t) {
+    uint32_t r = 0u, nx = 0xFFFFu;
 #pragma unroll
     for (int a = 0; a < N; ++a) {
       const uint32_t c0 = win[a] & 0xFFFFu, c1 = win[a] >> 16;
       r |= (c0 <= (uint32_t)t && (uint32_t)t < c1) ? (1u << a) : 0u;
+      const uint32_t b = (c0 > (uint32_t)t) ? c0 : ((c1 > (uint32_t)t) ? c1 : 0xFFFFu);
+      nx = b < nx ? b : nx;
     }
-    return r;
+    iso = r;
+    iso_next = nx;
   }
 
   // the Tick bits of step t
@@ -294,13 +312,14 @@ struct EvLane {
     m.st(S::WHEEL + S::WW * slot, 0u);
     occ &= ~(1u << slot);
     acc_mask = wq;
-    in_mask = wi | ticks_at(t);
+    // Ticks only up to the last skew; isolation changes only at window edges
+    in_mask = wi | ((t <= last_tick) ? ticks_at(t) : 0u);
 #pragma unroll
     for (int p = 0; p < PM; ++p) {
       const uint32_t grp = ((1u << (N + 1)) - 1u) << (p * (N + 1));
       canon += (in_mask & grp) ? 48u : 0u;
     }
-    if (crashy) iso = iso_at(t);
+    if (crashy && (uint32_t)t >= iso_next) iso_update(t);
   }
 
   // ---- instance start: parameters, Tick skews, isolation windows (SEMANTICS §4) ----
@@ -335,8 +354,7 @@ struct EvLane {
       const uint32_t wp = (p == 0) ? wsk.x : (p == 1) ? wsk.y : wsk.z;
       skew[p] = (kp.skew_max > 0u) ? mulhi_n(wp, kp.skew_max + 1u) : 0u;
       if ((uint32_t)p < P) last_tick = ((int32_t)skew[p] > last_tick) ? (int32_t)skew[p] : last_tick;
-      ticket[p] = cmd[p] = acks[p] = mr_t[p] = mr_v[p] = r2_v[p] = pending[p] = 0u;
-      rs[p] = IDLE;
+      pw0[p] = pw1[p] = 0u;                        // ticket 0, Idle, no command (Client.hs:90-95)
       nsent[p] = bnext[p] = refc[p] = 0u;
     }
     bool anyiso = false;
@@ -370,28 +388,33 @@ struct EvLane {
     clog_len = 0u;
     occ = 0u;
     iso = 0u;
+    iso_next = 0u;
     bailed = false;
     mode = M_RUN;
     enter(0);
   }
 
-  // broadcast o = (kind, x, z) by proposer q: bookkeeping of bcast() (oracle)
-  // and a pending entry whose N copies go out one per iteration
-  __host__ __device__ __forceinline__ void broadcast(uint32_t q, uint32_t kind, uint32_t x, uint32_t z, bool pred) {
-    rounds += (pred && kind == ASK) ? 1u : 0u;
-    const bool ex = pred && kind == EXECUTE;
+  // The handler's broadcasts (kind0, x0, z0) [and the restart's AskForTicket
+  // x1, Client.hs:185, only after an Execute] by proposer q: bookkeeping of
+  // bcast() (oracle) and pending entries whose N copies go out over the next
+  // iterations.  Payloads go to the next ring slots of q.
+  __host__ __device__ __forceinline__ void broadcast(uint32_t q, uint32_t kind0, uint32_t x0, uint32_t z0, bool p0,
+                                                     uint32_t x1, bool p1, uint32_t val) {
+    rounds += ((p0 && kind0 == ASK) ? 1u : 0u) + (p1 ? 1u : 0u);
+    const bool ex = p0 && kind0 == EXECUTE;
     execs += ex ? 1u : 0u;
-    if (ex && dval == 0u) {                          // the decided value: first Execute (Client.hs:178)
-      dval = get(r2_v, q);
-      dtick = x;
-    }
-    const uint32_t slot = get(bnext, q);
-    const uint32_t busy = (get(refc, q) >> (4u * slot)) & 15u;
-    bailed = bailed || (pred && busy != 0u);         // ring slot still referenced by a queued copy
-    m.st16(pred ? S::BRING : S::DUMMY, pred ? q * BR + slot : 0u, x | (z << 12) | (kind << 14));
-    pq |= pred ? ((q << 3) | slot) << (5u * pq_len) : 0u;
-    pq_len += pred ? 1u : 0u;
-    set(bnext, q, (slot + 1u) & (BR - 1u), pred);
+    const bool first = ex && dval == 0u;             // the decided value: first Execute (Client.hs:178)
+    dval = first ? val : dval;
+    dtick = first ? x0 : dtick;
+    const uint32_t slot0 = get(bnext, q), slot1 = (slot0 + 1u) & (BR - 1u);
+    const uint32_t rc = get(refc, q);
+    // a ring slot still referenced by a queued copy
+    bailed = bailed || (p0 && ((rc >> (4u * slot0)) & 15u) != 0u) || (p1 && ((rc >> (4u * slot1)) & 15u) != 0u);
+    m.st16(p0 ? S::BRING : S::DUMMY, p0 ? q * BR + slot0 : 0u, x0 | (z0 << 12) | (kind0 << 14));
+    m.st16(p1 ? S::BRING : S::DUMMY, p1 ? q * BR + slot1 : 0u, x1 | (ASK << 14));
+    pq |= (p0 ? ((q << 3) | slot0) << (5u * pq_len) : 0u) | (p1 ? ((q << 3) | slot1) << (5u * pq_len + 5u) : 0u);
+    pq_len += (p0 ? 1u : 0u) + (p1 ? 1u : 0u);
+    set(bnext, q, (slot0 + (p0 ? 1u : 0u) + (p1 ? 1u : 0u)) & (BR - 1u), p0);
   }
 
   // the next copy of the oldest pending broadcast, on link cp -> ca (Philox
@@ -563,8 +586,9 @@ struct EvLane {
       const uint32_t rkind = pe >> 30, px = pe & 0xFFFu, py = (pe >> 12) & 0xFFFu, pz = (pe >> 24) & 3u;
       canon += resp ? 2u * (16u >> rkind) : 0u;         // Round1OK 16, HaveTicket 8, Round2Success 4
 
-      uint32_t T = get(ticket, q), R = get(rs, q), K = get(acks, q);
-      uint32_t MT = get(mr_t, q), MV = get(mr_v, q), C2 = get(r2_v, q), PD = get(pending, q), CM = get(cmd, q);
+      const uint32_t w0 = get(pw0, q), w1 = get(pw1, q);
+      const uint32_t T = w0 & 0xFFFu, MT = (w0 >> 12) & 0xFFFu, K = (w0 >> 24) & 15u, R = (w0 >> 28) & 3u;
+      const uint32_t PD = (w0 >> 30) & 1u, MV = w1 & 3u, C2 = (w1 >> 2) & 3u, CM = (w1 >> 4) & 3u;
       uint32_t k0o = NONE, x0o = 0, z0o = 0;
       bool b1 = false;                                // the restart's AskForTicket (Client.hs:185)
       const uint32_t maj = (uint32_t)N >> 1;          // haveMajority: acks > floor(N/2), :191-194
@@ -589,16 +613,15 @@ struct EvLane {
       const uint32_t C2n = o_maj ? ((mv == 0u) ? CM : mv) : C2;    // Q5: pending whenever mr is Just
       z0o = C2n;
       b1 = s_maj && PD != 0u;
-      set(ticket, q, Tn, pin);
-      set(rs, q, restart ? ROUND1 : o_maj ? ROUND2 : (s_maj ? IDLE : R), pin);
-      set(acks, q, (restart || o_maj || s_maj) ? 0u : ((o_go || s_go) ? K1 : K), pin);
-      set(mr_t, q, (restart || o_maj) ? 0u : (o_go ? mt : MT), pin);
-      set(mr_v, q, (restart || o_maj) ? 0u : (o_go ? mv : MV), pin);
-      set(r2_v, q, C2n, pin);
-      set(pending, q, o_maj ? ((mv != 0u) ? 1u : 0u) : PD, pin);
-      set(cmd, q, t_go ? q + 1u : (s_maj && !PD) ? 0u : CM, pin);
-      broadcast(q, k0o, x0o, z0o, k0o != NONE);
-      broadcast(q, ASK, Tn, 0u, b1);
+      const uint32_t Rn = restart ? ROUND1 : o_maj ? ROUND2 : (s_maj ? IDLE : R);
+      const uint32_t Kn = (restart || o_maj || s_maj) ? 0u : ((o_go || s_go) ? K1 : K);
+      const uint32_t MTn = (restart || o_maj) ? 0u : (o_go ? mt : MT);
+      const uint32_t MVn = (restart || o_maj) ? 0u : (o_go ? mv : MV);
+      const uint32_t PDn = o_maj ? ((mv != 0u) ? 1u : 0u) : PD;
+      const uint32_t CMn = t_go ? q + 1u : (s_maj && !PD) ? 0u : CM;
+      set(pw0, q, Tn | (MTn << 12) | (Kn << 24) | (Rn << 28) | (PDn << 30), pin);
+      set(pw1, q, MVn | (C2n << 2) | (CMn << 4), pin);
+      broadcast(q, k0o, x0o, z0o, k0o != NONE, Tn, b1, C2n);
     }
   }
 
@@ -634,7 +657,7 @@ struct EvLane {
     uint32_t f = lflags | (capped ? (uint32_t)PXB_F_STEP_CAP : 0u) | (dval ? 0u : (uint32_t)PXB_F_UNDECIDED);
 #pragma unroll
     for (int p = 0; p < PM; ++p)
-      f |= (!capped && (uint32_t)p < P && rs[p] != IDLE) ? (uint32_t)PXB_F_STUCK : 0u;
+      f |= (!capped && (uint32_t)p < P && p_state(p) != IDLE) ? (uint32_t)PXB_F_STUCK : 0u;
     canon += 16u + 4u * (uint32_t)N;
     o.res[0] = dval ? ((dval << 24) | 1u) : 0u;
     o.res[1] = dval ? dtick : 0u;

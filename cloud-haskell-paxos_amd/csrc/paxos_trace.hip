@@ -30,14 +30,14 @@ __device__ void trace_record(const EvLane<PM, N, POOL, W, false, Mem>& L, uint32
     pxb_trace_prop q = {0, 0, 0, 0, 0, 0, 0, 0};
     if (p < PM && (uint32_t)p < L.P) {
       const uint32_t code = 1u;   // every command is c<id>.1 (docs/SEMANTICS.md §2)
-      q.ticket = (int32_t)L.ticket[p];
-      q.cmd = L.cmd[p] ? ((L.cmd[p] << 24) | code) : 0u;
-      q.acks = L.acks[p];
-      q.state = L.rs[p];
-      q.mr_t = (int32_t)L.mr_t[p];
-      q.mr_v = L.mr_v[p] ? ((L.mr_v[p] << 24) | code) : 0u;
-      q.r2_v = L.r2_v[p] ? ((L.r2_v[p] << 24) | code) : 0u;
-      q.pending = L.pending[p];
+      q.ticket = (int32_t)L.p_ticket(p);
+      q.cmd = L.p_cmd(p) ? ((L.p_cmd(p) << 24) | code) : 0u;
+      q.acks = L.p_acks(p);
+      q.state = L.p_state(p);
+      q.mr_t = (int32_t)L.p_mr_t(p);
+      q.mr_v = L.p_mr_v(p) ? ((L.p_mr_v(p) << 24) | code) : 0u;
+      q.r2_v = L.p_r2_v(p) ? ((L.p_r2_v(p) << 24) | code) : 0u;
+      q.pending = L.p_pending(p);
     }
     r->prop[p] = q;
   }
