@@ -30,9 +30,7 @@ constexpr uint32_t IDLE = 0, ROUND1 = 1, ROUND2 = 2;
 // two v_xor_b32 for it
 __host__ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  uint32_t r;
-  __asm__("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(c));
-  return r;
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);   // one v_bitop3_b32 (truth table of a^b^c)
 #else
   return a ^ b ^ c;
 #endif

@@ -55,11 +55,11 @@
 
 #include "../../include/paxos_batch.h"
 #include "paxos_device.h"
+#include "paxos_ev_sel.h"
 
 namespace pxb {
 namespace ev {
 
-constexpr uint32_t BR = 8;        // broadcast ring slots per proposer
 constexpr uint32_t PQ_CAP = 4;    // pending broadcasts per lane
 constexpr uint32_t MAX_STEP_CAP = 4095;   // 12-bit tickets (tickets <= step_cap, SEMANTICS §6)
 static_assert(MAX_STEP_CAP < PXB_TICKET_LIMIT, "EV tickets never reach the overflow limit");
@@ -87,10 +87,13 @@ struct Shape {
   static constexpr int RSEQ = REQ + NLQ;             // !CMP: NLQ halfwords of reply seq, index a*PM + p
   static constexpr int RSP = RSEQ + (CMP ? 0 : (NLQ + 1) / 2);   // NLQ response links, index p*N + a
   static constexpr int POOLW = RSP + NLQ;            // POOL response words
+  // broadcast ring slots per proposer: short-delay (compact) schedules never
+  // hold more than 4 broadcasts of one proposer in flight (BASELINE configs
+  // 3 and 4: the bail rate is the same with 4 slots as with 8)
+  static constexpr uint32_t BR = CMP ? 4 : 8;
   static constexpr int BRING = POOLW + POOL;         // PM*BR halfwords: broadcast payloads
   static constexpr int WHEEL = BRING + PM * BR / 2;  // W * WW due masks
-  static constexpr int DUMMY = WHEEL + W * WW;       // 1: target of the stores of inactive lanes
-  static constexpr int WORDS = DUMMY + 1;
+  static constexpr int WORDS = WHEEL + W * WW;
   static_assert(W == 8 || W == 16, "wheel of 8 or 16 steps");
   static_assert(NIN <= 32 && NLQ <= 32, "masks are 32-bit");
   static_assert(RD + 4 <= 32, "response-link word");
@@ -144,6 +147,9 @@ struct EvOut {
 #ifndef PXB_EV_CPOST
 #define PXB_EV_CPOST 1
 #endif
+#ifndef PXB_EV_SELBLK
+#define PXB_EV_SELBLK 0     // selects as one asm block each (paxos_ev_sel.h)
+#endif
 #ifndef PXB_EV_ACCN
 #define PXB_EV_ACCN 1       // acceptor ops per iteration
 #endif
@@ -163,13 +169,11 @@ struct EvLane {
   uint32_t gid;                       // instance index within the launch
   uint32_t lo, hi;                    // global instance id (Philox counter words 0, 1)
   uint32_t P, dmax, loss_m1;
-  bool lossy, faulty, crashy;
+  bool lossy, faulty;
   int32_t s, last_tick;
   uint32_t acc_mask;                  // this step's request links with due messages left
   uint32_t in_mask;                   // this step's proposer inputs left (Tick / response links)
   uint32_t occ;                       // wheel slots holding due bits
-  uint32_t iso;                       // acceptors isolated at step s
-  uint32_t iso_next;                  // the next step at which iso changes
   // proposer states (ClientState, Client.hs:58-67), packed (tickets < 2^12,
   // commands = clientId, acks <= N/2 + 1):
   //   pw0 = ticket [11:0] | mr_t [23:12] | acks [27:24] | state [29:28] | pending [30]
@@ -245,7 +249,11 @@ struct EvLane {
   }
   template <int K>
   __host__ __device__ static __forceinline__ uint32_t get(const uint32_t (&v)[K], uint32_t q) {
+#if defined(__HIP_DEVICE_COMPILE__) && PXB_EV_SELBLK
+    return Sel<K>::get(v, 1u << q);
+#else
     return get_from<K>(v, 1u << q, v[0]);
+#endif
   }
   template <int K, int I = 0>
   __host__ __device__ static __forceinline__ void set_from(uint32_t (&v)[K], uint32_t oh, uint32_t x) {
@@ -256,7 +264,11 @@ struct EvLane {
   }
   template <int K>
   __host__ __device__ static __forceinline__ void set(uint32_t (&v)[K], uint32_t q, uint32_t x, bool pred) {
+#if defined(__HIP_DEVICE_COMPILE__) && PXB_EV_SELBLK
+    Sel<K>::set(v, pred ? (1u << q) : 0u, x);
+#else
     set_from<K>(v, pred ? (1u << q) : 0u, x);
+#endif
   }
 
   // fields of the packed proposer state of p (finish, trace)
@@ -272,20 +284,6 @@ struct EvLane {
   __host__ __device__ __forceinline__ uint32_t rsp_ld(uint32_t Lr) const { return m.ld(S::RSP + Lr); }
   __host__ __device__ __forceinline__ void rsp_st(uint32_t Lr, uint32_t v) const { m.st(S::RSP + Lr, v); }
 
-  // the isolated acceptors at step t, and the next step at which that set changes
-  __host__ __device__ __forceinline__ void iso_update(int32_t t) {
-    uint32_t r = 0u, nx = 0xFFFFu;
-#pragma unroll
-    for (int a = 0; a < N; ++a) {
-      const uint32_t c0 = win[a] & 0xFFFFu, c1 = win[a] >> 16;
-      r |= (c0 <= (uint32_t)t && (uint32_t)t < c1) ? (1u << a) : 0u;
-      const uint32_t b = (c0 > (uint32_t)t) ? c0 : ((c1 > (uint32_t)t) ? c1 : 0xFFFFu);
-      nx = b < nx ? b : nx;
-    }
-    iso = r;
-    iso_next = nx;
-  }
-
   // the Tick bits of step t
   __host__ __device__ __forceinline__ uint32_t ticks_at(int32_t t) const {
     uint32_t r = 0u;
@@ -294,7 +292,7 @@ struct EvLane {
     return r;
   }
 
-  // enter step t: its due links from the wheel, its Ticks, its isolated acceptors;
+  // enter step t: its due links from the wheel, its Ticks;
   // 48 canonical bytes per proposer with an input (SEMANTICS §8)
   __host__ __device__ __forceinline__ void enter(int32_t t) {
     s = t;
@@ -312,14 +310,13 @@ struct EvLane {
     m.st(S::WHEEL + S::WW * slot, 0u);
     occ &= ~(1u << slot);
     acc_mask = wq;
-    // Ticks only up to the last skew; isolation changes only at window edges
+    // Ticks only up to the last skew
     in_mask = wi | ((t <= last_tick) ? ticks_at(t) : 0u);
 #pragma unroll
     for (int p = 0; p < PM; ++p) {
       const uint32_t grp = ((1u << (N + 1)) - 1u) << (p * (N + 1));
       canon += (in_mask & grp) ? 48u : 0u;
     }
-    if (crashy && (uint32_t)t >= iso_next) iso_update(t);
   }
 
   // ---- instance start: parameters, Tick skews, isolation windows (SEMANTICS §4) ----
@@ -331,7 +328,7 @@ struct EvLane {
     P = kp.n_prop;
     dmax = kp.delay_max;
     lossy = (kp.cfg & EV_CFG_LOSSY) != 0u;
-    crashy = (kp.cfg & EV_CFG_CRASHY) != 0u;
+    bool crashy = (kp.cfg & EV_CFG_CRASHY) != 0u;
     loss_m1 = kp.loss_m1;
     uint32_t crash_m1 = kp.crash_m1;
     if (kp.cfg & EV_CFG_RANDOMIZE) {                  // config-5 fuzz (SEMANTICS §4)
@@ -352,12 +349,11 @@ struct EvLane {
 #pragma unroll
     for (int p = 0; p < PM; ++p) {
       const uint32_t wp = (p == 0) ? wsk.x : (p == 1) ? wsk.y : wsk.z;
-      skew[p] = (kp.skew_max > 0u) ? mulhi_n(wp, kp.skew_max + 1u) : 0u;
-      if ((uint32_t)p < P) last_tick = ((int32_t)skew[p] > last_tick) ? (int32_t)skew[p] : last_tick;
+      skew[p] = (kp.skew_max > 0u && (uint32_t)p < P) ? mulhi_n(wp, kp.skew_max + 1u) : 0u;
+      last_tick = ((int32_t)skew[p] > last_tick) ? (int32_t)skew[p] : last_tick;
       pw0[p] = pw1[p] = 0u;                        // ticket 0, Idle, no command (Client.hs:90-95)
       nsent[p] = bnext[p] = refc[p] = 0u;
     }
-    bool anyiso = false;
 #pragma unroll
     for (int a = 0; a < N; ++a) {
       uint32_t c0 = 0, c1 = 0;
@@ -370,12 +366,10 @@ struct EvLane {
       }
       c0 = c0 < 4096u ? c0 : 4096u;
       c1 = c1 < 4096u ? c1 : 4096u;
-      anyiso = anyiso || c1 > c0;
       win[a] = c0 | (c1 << 16);
       accw[a] = 0u;
       accd[a] = 0x811C9DC5u;
     }
-    crashy = anyiso;                                 // no window at all: skip the isolation test
 #pragma unroll
     for (int i = S::REQ; i < S::POOLW; ++i) m.st(i, 0u);     // request links, reply seqs, response links
 #pragma unroll
@@ -387,8 +381,6 @@ struct EvLane {
     clog = 0ull;
     clog_len = 0u;
     occ = 0u;
-    iso = 0u;
-    iso_next = 0u;
     bailed = false;
     mode = M_RUN;
     enter(0);
@@ -406,15 +398,17 @@ struct EvLane {
     const bool first = ex && dval == 0u;             // the decided value: first Execute (Client.hs:178)
     dval = first ? val : dval;
     dtick = first ? x0 : dtick;
-    const uint32_t slot0 = get(bnext, q), slot1 = (slot0 + 1u) & (BR - 1u);
+    const uint32_t slot0 = get(bnext, q), slot1 = (slot0 + 1u) & (S::BR - 1u);
     const uint32_t rc = get(refc, q);
     // a ring slot still referenced by a queued copy
     bailed = bailed || (p0 && ((rc >> (4u * slot0)) & 15u) != 0u) || (p1 && ((rc >> (4u * slot1)) & 15u) != 0u);
-    m.st16(p0 ? S::BRING : S::DUMMY, p0 ? q * BR + slot0 : 0u, x0 | (z0 << 12) | (kind0 << 14));
-    m.st16(p1 ? S::BRING : S::DUMMY, p1 ? q * BR + slot1 : 0u, x1 | (ASK << 14));
+    if (p0) {                                        // (p1 only with p0)
+      m.st16(S::BRING, q * S::BR + slot0, x0 | (z0 << 12) | (kind0 << 14));
+      if (p1) m.st16(S::BRING, q * S::BR + slot1, x1 | (ASK << 14));
+    }
     pq |= (p0 ? ((q << 3) | slot0) << (5u * pq_len) : 0u) | (p1 ? ((q << 3) | slot1) << (5u * pq_len + 5u) : 0u);
     pq_len += (p0 ? 1u : 0u) + (p1 ? 1u : 0u);
-    set(bnext, q, (slot0 + (p0 ? 1u : 0u) + (p1 ? 1u : 0u)) & (BR - 1u), p0);
+    set(bnext, q, (slot0 + (p0 ? 1u : 0u) + (p1 ? 1u : 0u)) & (S::BR - 1u), p0);
   }
 
   // the next copy of the oldest pending broadcast, on link cp -> ca (Philox
@@ -450,10 +444,11 @@ struct EvLane {
     const uint32_t rel = qlen ? (((wq >> (7u * (qlen - 1u) + 3u)) & 15u) - s4) & 15u : 0u;
     const uint32_t due_rel = d > rel ? d : rel;
     const uint32_t ent = cslot | (((s4 + due_rel) & 15u) << 3);
-    m.st(go ? S::REQ + Lq : S::DUMMY, (wq & ~(QLM << S::QL)) | (ent << (7u * qlen)) | ((qlen + 1u) << S::QL));
+    // (inactive lanes store their word back unchanged)
+    m.st(S::REQ + Lq, go ? (wq & ~(QLM << S::QL)) | (ent << (7u * qlen)) | ((qlen + 1u) << S::QL) : wq);
     set(refc, cp, get(refc, cp) + (1u << (4u * cslot)), go);
     const uint32_t slot = ((uint32_t)s + due_rel) & WM;
-    m.orw(go ? S::WHEEL + slot * S::WW : S::DUMMY, 1u << Lq);
+    m.orw(S::WHEEL + slot * S::WW, go ? 1u << Lq : 0u);
     occ |= go ? (1u << slot) : 0u;
     in_flight += go ? 1u : 0u;
   }
@@ -485,12 +480,14 @@ struct EvLane {
     const bool keep = len > 1u && ((rq2 >> 3) & 15u) == s4;
     acc_mask = (acc && !keep) ? (acc_mask & ~(1u << L)) : acc_mask;
     in_flight -= acc ? 1u : 0u;
-    const uint32_t w16 = m.ld16(S::BRING, p * BR + bslot);
+    const uint32_t w16 = m.ld16(S::BRING, p * S::BR + bslot);
     set(refc, p, get(refc, p) - (1u << (4u * bslot)), acc);
     const uint32_t kind = w16 >> 14, x = w16 & 0xFFFu, z = (w16 >> 12) & 3u;
     const uint32_t A = get(accw, a);
     const bool dead = ((A >> 26) & 1u) != 0u;
-    const bool live = acc && !dead && !((iso >> a) & 1u);
+    const uint32_t wa = get(win, a);                 // isolated at s: c0 <= s < c1 (SEMANTICS §4)
+    const bool isol = (wa & 0xFFFFu) <= (uint32_t)s && (uint32_t)s < (wa >> 16);
+    const bool live = acc && !dead && !isol;
     const uint32_t rb = (kind == PROPOSE) ? 12u : 8u;
     canon += acc ? (live ? 2u * rb + 32u : rb) : 0u;
     const uint32_t t_max = A & 0xFFFu, t_store = (A >> 12) & 0xFFFu, val = (A >> 24) & 3u;
@@ -523,7 +520,7 @@ struct EvLane {
     set(accw, a, nt_max | (nt_store << 12) | (nval << 24) | ((dead || panic) ? (1u << 26) : 0u) | (log_len << 27),
         live);
     const bool snd1 = live && !is_exec;              // the reply, on link a -> p
-    m.st(acc ? S::REQ + L : S::DUMMY, rq2 | (S::CMP ? ((kr + (snd1 ? 1u : 0u)) << S::KSH) : 0u));
+    m.st(S::REQ + L, acc ? rq2 | (S::CMP ? ((kr + (snd1 ? 1u : 0u)) << S::KSH) : 0u) : wq);
 
     // ================= the reply, on a -> p (SEMANTICS §5) =================
     // Philox seq = the link's reply count.  Sent before the proposer part so its
@@ -534,7 +531,7 @@ struct EvLane {
     const uint32_t d1 = faulty ? 1u + mulhi_n(w1.y, dmax) : 1u;
     msgs += snd1 ? 1u : 0u;
     bailed = bailed || (snd1 && kr == (S::CMP ? (1u << S::KB) - 1u : 0xFFFFu));
-    if (!S::CMP) m.st16(snd1 ? S::RSEQ : S::DUMMY, snd1 ? L : 0u, kr + 1u);
+    if (!S::CMP) m.st16(S::RSEQ, L, snd1 ? kr + 1u : kr);
     {
       // enqueue (predicated: inactive lanes store to the dummy word)
       const bool go = snd1 && ok1;
@@ -547,12 +544,15 @@ struct EvLane {
       const uint32_t due4 = (s4 + due_rel) & 15u;
       const uint32_t k2 = (POOL > 32) ? (uint32_t)__builtin_ctzll((unsigned long long)pfree | (1ull << 63))
                                       : ctz32((uint32_t)pfree) & 31u;
+      // inactive lanes: the pool word goes to a free entry, or, with none
+      // free, to the link word, which the next store writes back unchanged
+      m.st(pfree ? S::POOLW + k2 : S::RSP + Lr, rx | (ry << 12) | (rz << 24) | (due4 << 26) | (rk << 30));
       pfree &= go ? ~((pool_mask_t)1 << k2) : ~(pool_mask_t)0;
-      m.st(go ? S::POOLW + k2 : S::DUMMY, rx | (ry << 12) | (rz << 24) | (due4 << 26) | (rk << 30));
-      m.st(go ? S::RSP + Lr : S::DUMMY, (rr & ((1u << (S::IB * rlen)) - 1u)) | (k2 << (S::IB * rlen)) |
-                                            ((rlen + 1u) << S::RL) | (due4 << S::RD));
+      m.st(S::RSP + Lr, go ? (rr & ((1u << (S::IB * rlen)) - 1u)) | (k2 << (S::IB * rlen)) | ((rlen + 1u) << S::RL) |
+                                 (due4 << S::RD)
+                           : rr);
       const uint32_t slot = ((uint32_t)s + due_rel) & WM;
-      m.orw(go ? S::WHEEL + slot * S::WW + (S::WW == 2 ? 1u : 0u) : S::DUMMY, 1u << (S::ISH + p * (N + 1) + 1u + a));
+      m.orw(S::WHEEL + slot * S::WW + (S::WW == 2 ? 1u : 0u), go ? 1u << (S::ISH + p * (N + 1) + 1u + a) : 0u);
       occ |= go ? (1u << slot) : 0u;
       in_flight += go ? 1u : 0u;
     }
@@ -578,8 +578,8 @@ struct EvLane {
       const uint32_t pe = m.ld(S::POOLW + k);
       const uint32_t pn = m.ld(S::POOLW + ((rr >> S::IB) & IM));
       pfree |= resp ? ((pool_mask_t)1 << k) : (pool_mask_t)0;
-      m.st(resp ? S::RSP + Lr : S::DUMMY, ((rr & ((1u << S::RL) - 1u)) >> S::IB) | ((rlen - 1u) << S::RL) |
-                                              (rr & (15u << S::RD)));
+      m.st(S::RSP + Lr, resp ? ((rr & ((1u << S::RL) - 1u)) >> S::IB) | ((rlen - 1u) << S::RL) | (rr & (15u << S::RD))
+                             : rr);
       const bool rkeep = resp && rlen > 1u && ((pn >> 26) & 15u) == s4;
       in_mask = (pin && !rkeep) ? (in_mask & ~(1u << j)) : in_mask;
       in_flight -= resp ? 1u : 0u;
@@ -630,20 +630,16 @@ struct EvLane {
   __host__ __device__ __forceinline__ bool end_op(const EvParams& kp, EvOut& o, bool act) {
     if (act && acc_mask == 0u && in_mask == 0u && pq_len == 0u) {
       const bool quiet = in_flight == 0u && s >= last_tick;
-      if (quiet) {
-        finish(false, o);
-        return true;
-      }
-      // the next step with a due message or a Tick
+      // the next step with a due message or a Tick (skews of absent proposers are 0)
       const uint32_t s1 = (uint32_t)s + 1u;
       const uint32_t rot = ((occ >> (s1 & WM)) | (occ << ((W - (s1 & WM)) & WM))) & ((1u << W) - 1u);
       uint32_t nx = occ ? s1 + ctz32(rot) : 0xFFFFu;
 #pragma unroll
-      for (int q = 0; q < PM; ++q)
-        nx = ((uint32_t)q < P && skew[q] > (uint32_t)s && skew[q] < nx) ? skew[q] : nx;
-      if (nx >= kp.step_cap) {
-        s = (int32_t)kp.step_cap - 1;
-        finish(true, o);
+      for (int q = 0; q < PM; ++q) nx = (skew[q] > (uint32_t)s && skew[q] < nx) ? skew[q] : nx;
+      const bool capped = !quiet && nx >= kp.step_cap;
+      if (quiet || capped) {
+        s = capped ? (int32_t)kp.step_cap - 1 : s;
+        finish(capped, o);
         return true;
       }
       enter((int32_t)nx);

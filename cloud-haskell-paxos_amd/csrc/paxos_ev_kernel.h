@@ -54,17 +54,21 @@ struct EvPool {
   static constexpr int value = (PM * N <= 16) ? (CMP ? 24 : 32) : (CMP ? 48 : 64);
 };
 
-// run totals kept per wave in LDS (added once per finished instance)
-constexpr int EV_NTOT = 11;
+// run totals added per finished instance (no-return global atomics into the
+// wave's partial row; finalize_kernel sums the rows)
+constexpr int EV_NTOT = 12;
+__device__ constexpr int tot_slot[EV_NTOT] = {PXB_C_INSTANCES, PXB_C_DECIDED, PXB_C_UNDECIDED, PXB_C_STUCK,
+                                              PXB_C_PANIC, PXB_C_DIVERGENCE, PXB_C_STEP_CAP, PXB_C_ROUNDS,
+                                              PXB_C_STEPS, PXB_C_MESSAGES, PXB_C_EXECUTES, PXB_C_CANON_BYTES};
 
 template <int PM, int N, int W, bool CMP>
 __global__ __launch_bounds__(64, 1) void paxos_ev_kernel(EvKParams kp) {
   constexpr int POOL = EvPool<PM, N, CMP>::value;
   using S = Shape<PM, N, POOL, W, CMP>;
   __shared__ uint32_t lds[S::WORDS * 64];
-  __shared__ unsigned long long wtot[16];
   const uint32_t lane = threadIdx.x;
-  if (lane < 16) wtot[lane] = 0ull;
+  // run totals: added per finished instance into this wave's partial row
+  unsigned long long* const trow = kp.part + (size_t)(blockIdx.x % EV_TCOPIES) * 16u;
   EvLane<PM, N, POOL, W, CMP, LdsMem> L;
   L.m = LdsMem{lds, lane};
   L.mode = M_IDLE;
@@ -109,6 +113,7 @@ __global__ __launch_bounds__(64, 1) void paxos_ev_kernel(EvKParams kp) {
       } else if (done) {
         const uint32_t f = o.flags;
         const uint32_t v[EV_NTOT] = {1u,
+                                     (f & PXB_F_UNDECIDED) ? 0u : 1u,
                                      (f & PXB_F_UNDECIDED) ? 1u : 0u,
                                      (f & PXB_F_STUCK) ? 1u : 0u,
                                      (f & PXB_F_PANIC) ? 1u : 0u,
@@ -121,7 +126,7 @@ __global__ __launch_bounds__(64, 1) void paxos_ev_kernel(EvKParams kp) {
                                      L.canon};
 #pragma unroll
         for (int q = 0; q < EV_NTOT; ++q)
-          if (v[q]) atomicAdd(&wtot[q], (unsigned long long)v[q]);
+          if (v[q]) atomicAdd(&trow[tot_slot[q]], (unsigned long long)v[q]);
         if (kp.out) kp.out[L.gid] = make_uint4(o.res[0], o.res[1], o.res[2], o.res[3]);
         if (kp.dig) {
 #pragma unroll
@@ -139,17 +144,6 @@ __global__ __launch_bounds__(64, 1) void paxos_ev_kernel(EvKParams kp) {
     }
   }
 
-  // ---- run totals: one atomic per counter into a partial row ----
-  __syncthreads();
-  unsigned long long* const trow = kp.part + (size_t)(blockIdx.x % EV_TCOPIES) * 16u;
-  if (lane < EV_NTOT) {
-    const int slot_of[EV_NTOT] = {PXB_C_INSTANCES, PXB_C_UNDECIDED, PXB_C_STUCK, PXB_C_PANIC, PXB_C_DIVERGENCE,
-                                  PXB_C_STEP_CAP, PXB_C_ROUNDS, PXB_C_STEPS, PXB_C_MESSAGES, PXB_C_EXECUTES,
-                                  PXB_C_CANON_BYTES};
-    const unsigned long long val = wtot[lane];
-    if (val) atomicAdd(&trow[slot_of[lane]], val);
-    if (lane == 0 && wtot[0] != wtot[1]) atomicAdd(&trow[PXB_C_DECIDED], wtot[0] - wtot[1]);
-  }
 }
 
 }  // namespace ev
