@@ -154,7 +154,10 @@ struct EvOut {
 #define PXB_EV_ACCN 1       // acceptor ops per iteration
 #endif
 
-template <int PM, int N, int POOL, int W, bool CMP, class Mem>
+// EARLY: a step may end with the copies of its last broadcast still to send
+// (see end_op); the trace kernel turns it off so that its per-step records
+// hold every message of the step in flight, as the oracle's do.
+template <int PM, int N, int POOL, int W, bool CMP, class Mem, bool EARLY = true>
 struct EvLane {
   using S = Shape<PM, N, POOL, W, CMP>;
   using pool_mask_t = typename std::conditional<(POOL > 32), unsigned long long, uint32_t>::type;
@@ -186,6 +189,8 @@ struct EvLane {
   // acceptor states (Server.hs:24-31), isolation windows, log digests
   uint32_t accw[N], win[N], accd[N];
   uint32_t pq, pq_len, acur;          // pending broadcasts (p << 3 | slot, 5 bits each), next acceptor
+  bool pq_old;                        // the head pending broadcast was made at step s - 1
+  uint32_t canon0;                    // canon on entering a step that carries one over (else canon - 1)
   pool_mask_t pfree;                  // free response-pool words
   uint32_t in_flight;
   uint32_t lflags, rounds, dval, dtick, execs, msgs, canon;
@@ -296,6 +301,8 @@ struct EvLane {
   // 48 canonical bytes per proposer with an input (SEMANTICS §8)
   __host__ __device__ __forceinline__ void enter(int32_t t) {
     s = t;
+    pq_old = pq_len != 0u;                           // (only ever one: end_op)
+    canon0 = pq_old ? canon : canon - 1u;
     const uint32_t slot = (uint32_t)t & WM;
     uint32_t wq, wi;
     if (S::WW == 1) {
@@ -375,6 +382,7 @@ struct EvLane {
 #pragma unroll
     for (int i = 0; i < W * S::WW; ++i) m.st(S::WHEEL + i, 0u);
     pq = pq_len = acur = 0u;
+    pq_old = false;
     pfree = full_pool();
     in_flight = 0u;
     lflags = rounds = dval = dtick = execs = msgs = canon = 0u;
@@ -415,7 +423,9 @@ struct EvLane {
   // seq = the broadcast index, the link's seq: every broadcast tries every acceptor)
   __host__ __device__ __forceinline__ bool copy_ready() const { return pq_len != 0u; }
   __host__ __device__ __forceinline__ void copy_send(const EvParams& kp, bool act) {
-    const uint32_t s4 = (uint32_t)s & 15u;
+    // the broadcast's own step: s, or s - 1 for one carried over by end_op
+    const uint32_t sb = (uint32_t)s - (pq_old ? 1u : 0u);
+    const uint32_t s4 = sb & 15u;
     const bool snd = act && pq_len != 0u;
     const uint32_t ce = pq & 31u;
     const uint32_t cp = ce >> 3, cslot = ce & 7u, ca = acur;
@@ -426,6 +436,7 @@ struct EvLane {
         pq >>= 5;
         pq_len -= 1u;
         acur = 0u;
+        pq_old = false;
         set(nsent, cp, ck + 1u, true);
       }
     }
@@ -447,9 +458,13 @@ struct EvLane {
     // (inactive lanes store their word back unchanged)
     m.st(S::REQ + Lq, go ? (wq & ~(QLM << S::QL)) | (ent << (7u * qlen)) | ((qlen + 1u) << S::QL) : wq);
     set(refc, cp, get(refc, cp) + (1u << (4u * cslot)), go);
-    const uint32_t slot = ((uint32_t)s + due_rel) & WM;
-    m.orw(S::WHEEL + slot * S::WW, go ? 1u << Lq : 0u);
-    occ |= go ? (1u << slot) : 0u;
+    // due at s (a carried-over copy with the shortest delay): straight into
+    // this step's due links, else into the wheel
+    const bool now = EARLY && sb + due_rel == (uint32_t)s;
+    const uint32_t slot = (sb + due_rel) & WM;
+    m.orw(S::WHEEL + slot * S::WW, (go && !now) ? 1u << Lq : 0u);
+    occ |= (go && !now) ? (1u << slot) : 0u;
+    acc_mask |= (go && now) ? (1u << Lq) : 0u;
     in_flight += go ? 1u : 0u;
   }
 
@@ -466,11 +481,17 @@ struct EvLane {
   }
 
   // ================= ACC: one due request (Server.hs:51-78) and its reply =================
-  __host__ __device__ __forceinline__ bool acc_ready() const { return acc_mask != 0u; }
+  __host__ __device__ __forceinline__ bool acc_ready() const {
+    return ((EARLY && pq_old) ? acc_mask & ((1u << (acur * (uint32_t)PM)) - 1u) : acc_mask) != 0u;
+  }
   __host__ __device__ __forceinline__ void acc_op(const EvParams& kp, bool act) {
     const uint32_t s4 = (uint32_t)s & 15u;
-    const bool acc = act && acc_mask != 0u;
-    const uint32_t L = acc ? ctz32(acc_mask) : 0u;
+    // while a carried-over broadcast has copies left, only the acceptors it
+    // has reached may run (its copy to acceptor a may be due now, and a takes
+    // its requests in (p, seq) order)
+    const uint32_t ready = (EARLY && pq_old) ? acc_mask & ((1u << (acur * (uint32_t)PM)) - 1u) : acc_mask;
+    const bool acc = act && ready != 0u;
+    const uint32_t L = acc ? ctz32(ready) : 0u;
     const uint32_t a = L / (uint32_t)PM, p = L - a * (uint32_t)PM;
     const uint32_t wq = m.ld(S::REQ + L);
     const uint32_t kr = S::CMP ? (wq >> S::KSH) : m.ld16(S::RSEQ, L);   // the reply's link sequence number
@@ -626,19 +647,29 @@ struct EvLane {
   }
 
   // ================= END of step: quiescence, step cap, next step =================
-  __host__ __device__ __forceinline__ bool end_ready() const { return acc_mask == 0u && in_mask == 0u && pq_len == 0u; }
+  // A step ends when its due messages and inputs are handled and its
+  // broadcasts' copies are sent, except for the copies of one broadcast of
+  // this step below the step cap: those go out during step s + 1 (next to
+  // its own work), which is then the next step whatever else is due.  Their
+  // delays are counted from s, so none is due before s + 1.
+  __host__ __device__ __forceinline__ bool end_ready(const EvParams& kp) const {
+    return acc_mask == 0u && in_mask == 0u &&
+           (pq_len == 0u || (EARLY && pq_len == 1u && !pq_old && (uint32_t)s + 1u < kp.step_cap));
+  }
   __host__ __device__ __forceinline__ bool end_op(const EvParams& kp, EvOut& o, bool act) {
-    if (act && acc_mask == 0u && in_mask == 0u && pq_len == 0u) {
-      const bool quiet = in_flight == 0u && s >= last_tick;
+    if (act && end_ready(kp)) {
+      const bool quiet = pq_len == 0u && in_flight == 0u && s >= last_tick;
+      // nothing but lost copies at a carried-over step: the instance was quiet at s - 1
+      const bool back = EARLY && canon == canon0;
       // the next step with a due message or a Tick (skews of absent proposers are 0)
       const uint32_t s1 = (uint32_t)s + 1u;
       const uint32_t rot = ((occ >> (s1 & WM)) | (occ << ((W - (s1 & WM)) & WM))) & ((1u << W) - 1u);
-      uint32_t nx = occ ? s1 + ctz32(rot) : 0xFFFFu;
+      uint32_t nx = (occ && pq_len == 0u) ? s1 + ctz32(rot) : (pq_len ? s1 : 0xFFFFu);
 #pragma unroll
       for (int q = 0; q < PM; ++q) nx = (skew[q] > (uint32_t)s && skew[q] < nx) ? skew[q] : nx;
       const bool capped = !quiet && nx >= kp.step_cap;
       if (quiet || capped) {
-        s = capped ? (int32_t)kp.step_cap - 1 : s;
+        s = capped ? (int32_t)kp.step_cap - 1 : (back ? s - 1 : s);
         finish(capped, o);
         return true;
       }

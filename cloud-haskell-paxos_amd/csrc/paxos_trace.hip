@@ -12,7 +12,7 @@ namespace pxb {
 namespace ev {
 
 template <int PM, int N, int POOL, int W, class Mem>
-__device__ void trace_record(const EvLane<PM, N, POOL, W, false, Mem>& L, uint32_t step, pxb_trace_step* r) {
+__device__ void trace_record(const EvLane<PM, N, POOL, W, false, Mem, false>& L, uint32_t step, pxb_trace_step* r) {
   r->step = step;
   r->in_flight = L.in_flight;
   r->n_acceptors = N;
@@ -52,7 +52,7 @@ __global__ __launch_bounds__(64) void paxos_trace_kernel(EvParams p, uint32_t gi
   using S = Shape<PM, N, POOL, W, false>;
   __shared__ uint32_t lds[S::WORDS * 64];
   if (threadIdx.x != 0) return;
-  EvLane<PM, N, POOL, W, false, LdsMem> L;
+  EvLane<PM, N, POOL, W, false, LdsMem, false> L;   // every step drains its copies: see EARLY
   L.m = LdsMem{lds, 0u};
   L.init(p, gid);
   uint32_t n = 0;
