@@ -52,6 +52,22 @@ __host__ __device__ __forceinline__ uint4 philox(uint32_t c0, uint32_t c1, uint3
   return make_uint4(c0, c1, c2, c3);
 }
 
+// the same with its 2 x 10 round keys precomputed: rk[2r], rk[2r+1] = the keys
+// of round r (k0 + r * 0x9E3779B9, k1 + r * 0xBB67AE85)
+__host__ __device__ __forceinline__ uint4 philox_rk(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                           const uint32_t (&rk)[20]) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)c0 * 0xD2511F53u, p1 = (uint64_t)c2 * 0xCD9E8D57u;
+    const uint32_t n0 = xor3((uint32_t)(p1 >> 32), c1, rk[2 * r]), n2 = xor3((uint32_t)(p0 >> 32), c3, rk[2 * r + 1]);
+    c1 = (uint32_t)p1;
+    c3 = (uint32_t)p0;
+    c0 = n0;
+    c2 = n2;
+  }
+  return make_uint4(c0, c1, c2, c3);
+}
+
 __host__ __device__ __forceinline__ uint32_t mulhi_n(uint32_t w, uint32_t n) {
   return (uint32_t)(((uint64_t)w * n) >> 32);   // v_mul_hi_u32 on the device
 }

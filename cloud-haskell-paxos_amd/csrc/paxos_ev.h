@@ -150,6 +150,9 @@ struct EvOut {
 #ifndef PXB_EV_SELBLK
 #define PXB_EV_SELBLK 0     // selects as one asm block each (paxos_ev_sel.h)
 #endif
+#ifndef PXB_EV_VKEYS
+#define PXB_EV_VKEYS 1      // Philox round keys precomputed in VGPRs (set_keys)
+#endif
 #ifndef PXB_EV_ACCN
 #define PXB_EV_ACCN 1       // acceptor ops per iteration
 #endif
@@ -167,6 +170,9 @@ struct EvLane {
   static constexpr uint32_t IM = (1u << S::IB) - 1u;
 
   Mem m;
+#if PXB_EV_VKEYS
+  uint32_t rk[20];                    // Philox round keys (set_keys): uniform, held in VGPRs
+#endif
   // ---- instance ----
   uint32_t mode;
   uint32_t gid;                       // instance index within the launch
@@ -326,6 +332,25 @@ struct EvLane {
     }
   }
 
+  // the launch's Philox round keys, once per wave: as VGPRs they cost no
+  // per-round key arithmetic, and (unlike 20 SGPRs) push nothing into spills
+  __host__ __device__ __forceinline__ void set_keys(const EvParams& kp) {
+#if PXB_EV_VKEYS
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+      rk[2 * r] = opaque(kp.k0 + (uint32_t)r * 0x9E3779B9u);
+      rk[2 * r + 1] = opaque(kp.k1 + (uint32_t)r * 0xBB67AE85u);
+    }
+#endif
+  }
+  __host__ __device__ __forceinline__ uint4 draw(uint32_t c2, uint32_t c3, const EvParams& kp) const {
+#if PXB_EV_VKEYS
+    return philox_rk(lo, hi, c2, c3, rk);
+#else
+    return philox(lo, hi, c2, c3, skey(kp.k0), skey(kp.k1));
+#endif
+  }
+
   // ---- instance start: parameters, Tick skews, isolation windows (SEMANTICS §4) ----
   __host__ __device__ __forceinline__ void init(const EvParams& kp, uint32_t g) {
     gid = g;
@@ -442,7 +467,7 @@ struct EvLane {
     }
     // the draw is computed unconditionally (a branch around it would keep
     // the iteration's three independent Philox chains from interleaving)
-    const uint4 w = philox(lo, hi, ck, (1u << 24) | (cp << 8) | ca, skey(kp.k0), skey(kp.k1));
+    const uint4 w = draw(ck, (1u << 24) | (cp << 8) | ca, kp);
     const bool ok = !(lossy && w.x <= loss_m1);
     const uint32_t d = faulty ? 1u + mulhi_n(w.y, dmax) : 1u;
     msgs += snd ? 1u : 0u;
@@ -547,7 +572,7 @@ struct EvLane {
     // Philox seq = the link's reply count.  Sent before the proposer part so its
     // state dies early; the proposer part only pops due-now heads, so the order
     // of the two on one link does not matter.
-    const uint4 w1 = philox(lo, hi, kr, (1u << 24) | (1u << 16) | (p << 8) | a, skey(kp.k0), skey(kp.k1));
+    const uint4 w1 = draw(kr, (1u << 24) | (1u << 16) | (p << 8) | a, kp);
     const bool ok1 = !(lossy && w1.x <= loss_m1);
     const uint32_t d1 = faulty ? 1u + mulhi_n(w1.y, dmax) : 1u;
     msgs += snd1 ? 1u : 0u;

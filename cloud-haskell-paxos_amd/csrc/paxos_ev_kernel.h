@@ -71,6 +71,7 @@ __global__ __launch_bounds__(64, 1) void paxos_ev_kernel(EvKParams kp) {
   unsigned long long* const trow = kp.part + (size_t)(blockIdx.x % EV_TCOPIES) * 16u;
   EvLane<PM, N, POOL, W, CMP, LdsMem> L;
   L.m = LdsMem{lds, lane};
+  L.set_keys(kp.p);
   L.mode = M_IDLE;
   L.bailed = false;
   const uint32_t n = kp.n_instances;

@@ -54,6 +54,7 @@ __global__ __launch_bounds__(64) void paxos_trace_kernel(EvParams p, uint32_t gi
   if (threadIdx.x != 0) return;
   EvLane<PM, N, POOL, W, false, LdsMem, false> L;   // every step drains its copies: see EARLY
   L.m = LdsMem{lds, 0u};
+  L.set_keys(p);
   L.init(p, gid);
   uint32_t n = 0;
   for (;;) {

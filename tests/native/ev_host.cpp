@@ -34,6 +34,7 @@ int run_shape(const pxb_config* cfg, pxb_result* out, uint32_t* dig, pxb_accepto
   const EvParams p = make_params(cfg);
   EvLane<PM, N, POOL, W, CMP, HostMem> L;
   L.m = HostMem{buf.data()};
+  L.set_keys(p);
   uint32_t nb = 0;
   uint64_t ms = 0;
   for (uint32_t g = 0; g < (uint32_t)cfg->n_instances; ++g) {

@@ -10,6 +10,6 @@ for c in 4 3 5; do
   python3 -c "import json; e=json.load(open('gpurun_out/q/c$c.json')); print('config $c: %.1f M/s  %.2f ms/step' % (e['value']/1e6, e['ms_per_step']))"
 done
 cd /tmp && export TMPDIR=/tmp
-CNT="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
+CNT="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_WAIT_ANY GRBM_GUI_ACTIVE"
 timeout -s KILL 120 rocprofv3 --pmc $CNT -d $R/gpurun_out/q/pmc4 -o pmc --output-format csv -- python3 $R/bench.py --no-cpu --no-extra --config 4 --instances 4194304 --steps 2 --warmup 1 > $R/gpurun_out/q/pmc4.log 2>&1 || exit 1
-cd $R && python3 tools/pmc_summary.py gpurun_out/q/pmc4 paxos_ev_kernel | grep -E "INSTS_VALU|INSTS_SALU|GRBM|WAVES "
+cd $R && python3 tools/pmc_summary.py gpurun_out/q/pmc4 paxos_ev_kernel | cat
