@@ -178,7 +178,7 @@ struct EvLane {
   uint32_t gid;                       // instance index within the launch
   uint32_t lo, hi;                    // global instance id (Philox counter words 0, 1)
   uint32_t P, dmax, loss_m1;
-  bool lossy, faulty;
+  bool lossy;
   int32_t s, last_tick;
   uint32_t acc_mask;                  // this step's request links with due messages left
   uint32_t in_mask;                   // this step's proposer inputs left (Tick / response links)
@@ -374,7 +374,6 @@ struct EvLane {
       crashy = ct != 0ull;
       crash_m1 = (uint32_t)(ct - 1ull);
     }
-    faulty = lossy || dmax > 1u;
     uint4 wsk = make_uint4(0, 0, 0, 0);
     if (kp.skew_max > 0u) wsk = philox(lo, hi, 0u, 2u << 24, kp.k0, kp.k1);
     last_tick = 0;
@@ -455,21 +454,20 @@ struct EvLane {
     const uint32_t ce = pq & 31u;
     const uint32_t cp = ce >> 3, cslot = ce & 7u, ca = acur;
     const uint32_t ck = get(nsent, cp);
-    if (snd) {
-      acur += 1u;
-      if (acur == (uint32_t)N) {
-        pq >>= 5;
-        pq_len -= 1u;
-        acur = 0u;
-        pq_old = false;
-        set(nsent, cp, ck + 1u, true);
-      }
+    {                                                // (branch-free: selects, no exec-mask branches)
+      const uint32_t a1 = acur + 1u;
+      const bool wrap = snd && a1 == (uint32_t)N;    // the broadcast's last copy
+      acur = wrap ? 0u : (snd ? a1 : acur);
+      pq = wrap ? pq >> 5 : pq;
+      pq_len -= wrap ? 1u : 0u;
+      pq_old = pq_old && !wrap;
+      set(nsent, cp, ck + 1u, wrap);
     }
     // the draw is computed unconditionally (a branch around it would keep
     // the iteration's three independent Philox chains from interleaving)
     const uint4 w = draw(ck, (1u << 24) | (cp << 8) | ca, kp);
     const bool ok = !(lossy && w.x <= loss_m1);
-    const uint32_t d = faulty ? 1u + mulhi_n(w.y, dmax) : 1u;
+    const uint32_t d = 1u + mulhi_n(w.y, dmax);      // (delay_max <= 1: always 1)
     msgs += snd ? 1u : 0u;
     // enqueue (predicated: inactive lanes store to the dummy word)
     const bool go = snd && ok;
@@ -477,7 +475,7 @@ struct EvLane {
     const uint32_t wq = m.ld(S::REQ + Lq);
     const uint32_t qlen = (wq >> S::QL) & QLM;
     bailed = bailed || (go && qlen >= (uint32_t)S::QC);
-    const uint32_t rel = qlen ? (((wq >> (7u * (qlen - 1u) + 3u)) & 15u) - s4) & 15u : 0u;
+    const uint32_t rel = (((wq >> ((7u * qlen - 4u) & 31u)) & 15u) - s4) & (qlen ? 15u : 0u);   // tail's due - sb
     const uint32_t due_rel = d > rel ? d : rel;
     const uint32_t ent = cslot | (((s4 + due_rel) & 15u) << 3);
     // (inactive lanes store their word back unchanged)
@@ -574,7 +572,7 @@ struct EvLane {
     // of the two on one link does not matter.
     const uint4 w1 = draw(kr, (1u << 24) | (1u << 16) | (p << 8) | a, kp);
     const bool ok1 = !(lossy && w1.x <= loss_m1);
-    const uint32_t d1 = faulty ? 1u + mulhi_n(w1.y, dmax) : 1u;
+    const uint32_t d1 = 1u + mulhi_n(w1.y, dmax);
     msgs += snd1 ? 1u : 0u;
     bailed = bailed || (snd1 && kr == (S::CMP ? (1u << S::KB) - 1u : 0xFFFFu));
     if (!S::CMP) m.st16(S::RSEQ, L, snd1 ? kr + 1u : kr);
@@ -585,7 +583,7 @@ struct EvLane {
       const uint32_t rr = rsp_ld(Lr);
       const uint32_t rlen = (rr >> S::RL) & RLM;
       bailed = bailed || (go && (rlen >= (uint32_t)S::RC || pfree == 0));
-      const uint32_t rel = rlen ? (((rr >> S::RD) & 15u) - s4) & 15u : 0u;
+      const uint32_t rel = (((rr >> S::RD) & 15u) - s4) & (rlen ? 15u : 0u);
       const uint32_t due_rel = d1 > rel ? d1 : rel;
       const uint32_t due4 = (s4 + due_rel) & 15u;
       const uint32_t k2 = (POOL > 32) ? (uint32_t)__builtin_ctzll((unsigned long long)pfree | (1ull << 63))
