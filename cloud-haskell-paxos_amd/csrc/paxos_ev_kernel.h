@@ -54,12 +54,45 @@ struct EvPool {
   static constexpr int value = (PM * N <= 16) ? (CMP ? 24 : 32) : (CMP ? 48 : 64);
 };
 
-// run totals added per finished instance (no-return global atomics into the
-// wave's partial row; finalize_kernel sums the rows)
-constexpr int EV_NTOT = 12;
-__device__ constexpr int tot_slot[EV_NTOT] = {PXB_C_INSTANCES, PXB_C_DECIDED, PXB_C_UNDECIDED, PXB_C_STUCK,
-                                              PXB_C_PANIC, PXB_C_DIVERGENCE, PXB_C_STEP_CAP, PXB_C_ROUNDS,
-                                              PXB_C_STEPS, PXB_C_MESSAGES, PXB_C_EXECUTES, PXB_C_CANON_BYTES};
+// Run totals: each lane sums its finished instances in registers; the wave
+// adds the lane sums into its partial row (finalize_kernel sums the rows)
+// when it ends, or earlier once a lane has summed EV_FLUSH instances, which
+// keeps every 32-bit sum from wrapping (an instance runs < 2^12 steps and
+// sends < 2^10 messages per step: at most 2^8 x 2^22; canonical bytes are
+// summed in 64 bits).
+constexpr int EV_NTOT = 11;
+constexpr uint32_t EV_FLUSH = 1u << 8;
+__device__ constexpr int tot_slot[EV_NTOT] = {PXB_C_INSTANCES, PXB_C_UNDECIDED, PXB_C_STUCK, PXB_C_PANIC,
+                                              PXB_C_DIVERGENCE, PXB_C_STEP_CAP, PXB_C_ROUNDS, PXB_C_STEPS,
+                                              PXB_C_MESSAGES, PXB_C_EXECUTES, PXB_C_CANON_BYTES};
+
+struct EvTotals {
+  uint32_t c[EV_NTOT - 1];            // the 32-bit sums, in tot_slot order
+  uint64_t canon;
+  __device__ void clear() {
+#pragma unroll
+    for (int q = 0; q < EV_NTOT - 1; ++q) c[q] = 0u;
+    canon = 0ull;
+  }
+  __device__ static uint64_t wave_sum(uint64_t v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+  }
+  // the wave's sums into its partial row (all 64 lanes of the wave call this)
+  __device__ void flush(unsigned long long* trow, uint32_t lane) {
+#pragma unroll
+    for (int q = 0; q < EV_NTOT - 1; ++q) {
+      const uint64_t t = wave_sum((uint64_t)c[q]);
+      if (lane == 0 && t) atomicAdd(&trow[tot_slot[q]], (unsigned long long)t);
+    }
+    const uint64_t t = wave_sum(canon);
+    if (lane == 0 && t) atomicAdd(&trow[PXB_C_CANON_BYTES], (unsigned long long)t);
+    const uint64_t d = wave_sum((uint64_t)(c[0] - c[1]));        // decided = instances - undecided
+    if (lane == 0 && d) atomicAdd(&trow[PXB_C_DECIDED], (unsigned long long)d);
+    clear();
+  }
+};
 
 template <int PM, int N, int W, bool CMP>
 __global__ __launch_bounds__(64, 1) void paxos_ev_kernel(EvKParams kp) {
@@ -67,8 +100,9 @@ __global__ __launch_bounds__(64, 1) void paxos_ev_kernel(EvKParams kp) {
   using S = Shape<PM, N, POOL, W, CMP>;
   __shared__ uint32_t lds[S::WORDS * 64];
   const uint32_t lane = threadIdx.x;
-  // run totals: added per finished instance into this wave's partial row
   unsigned long long* const trow = kp.part + (size_t)(blockIdx.x % EV_TCOPIES) * 16u;
+  EvTotals tot;
+  tot.clear();
   EvLane<PM, N, POOL, W, CMP, LdsMem> L;
   L.m = LdsMem{lds, lane};
   L.set_keys(kp.p);
@@ -83,6 +117,8 @@ __global__ __launch_bounds__(64, 1) void paxos_ev_kernel(EvKParams kp) {
     // ---- refill idle lanes from the wave's chunk of the queue ----
     uint64_t freeb = __builtin_amdgcn_ballot_w64(L.mode == M_IDLE);
     while (freeb != 0ull && !drained) {
+      // (wave-uniform; a lane's sums only grow by instances it takes here)
+      if (__builtin_amdgcn_ballot_w64(tot.c[0] >= EV_FLUSH) != 0ull) tot.flush(trow, lane);
       if (next >= end) {
         uint32_t c = 0;
         if (lane == 0) c = atomicAdd(kp.queue, EV_QCHUNK);
@@ -113,21 +149,17 @@ __global__ __launch_bounds__(64, 1) void paxos_ev_kernel(EvKParams kp) {
         L.bailed = false;
       } else if (done) {
         const uint32_t f = o.flags;
-        const uint32_t v[EV_NTOT] = {1u,
-                                     (f & PXB_F_UNDECIDED) ? 0u : 1u,
-                                     (f & PXB_F_UNDECIDED) ? 1u : 0u,
-                                     (f & PXB_F_STUCK) ? 1u : 0u,
-                                     (f & PXB_F_PANIC) ? 1u : 0u,
-                                     (f & PXB_F_LOG_DIVERGENCE) ? 1u : 0u,
-                                     (f & PXB_F_STEP_CAP) ? 1u : 0u,
-                                     L.rounds,
-                                     o.steps,
-                                     L.msgs,
-                                     L.execs,
-                                     L.canon};
-#pragma unroll
-        for (int q = 0; q < EV_NTOT; ++q)
-          if (v[q]) atomicAdd(&trow[tot_slot[q]], (unsigned long long)v[q]);
+        tot.c[0] += 1u;
+        tot.c[1] += (f & PXB_F_UNDECIDED) ? 1u : 0u;
+        tot.c[2] += (f & PXB_F_STUCK) ? 1u : 0u;
+        tot.c[3] += (f & PXB_F_PANIC) ? 1u : 0u;
+        tot.c[4] += (f & PXB_F_LOG_DIVERGENCE) ? 1u : 0u;
+        tot.c[5] += (f & PXB_F_STEP_CAP) ? 1u : 0u;
+        tot.c[6] += L.rounds;
+        tot.c[7] += o.steps;
+        tot.c[8] += L.msgs;
+        tot.c[9] += L.execs;
+        tot.canon += L.canon;
         if (kp.out) kp.out[L.gid] = make_uint4(o.res[0], o.res[1], o.res[2], o.res[3]);
         if (kp.dig) {
 #pragma unroll
@@ -144,7 +176,7 @@ __global__ __launch_bounds__(64, 1) void paxos_ev_kernel(EvKParams kp) {
       }
     }
   }
-
+  tot.flush(trow, lane);
 }
 
 }  // namespace ev
