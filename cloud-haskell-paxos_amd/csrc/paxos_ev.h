@@ -433,7 +433,8 @@ struct EvLane {
     const uint32_t slot0 = get(bnext, q), slot1 = (slot0 + 1u) & (S::BR - 1u);
     const uint32_t rc = get(refc, q);
     // a ring slot still referenced by a queued copy
-    bailed = bailed || (p0 && ((rc >> (4u * slot0)) & 15u) != 0u) || (p1 && ((rc >> (4u * slot1)) & 15u) != 0u);
+    // (non-short-circuit: || here became two exec-mask branches)
+    bailed = bailed | (p0 & (((rc >> (4u * slot0)) & 15u) != 0u)) | (p1 & (((rc >> (4u * slot1)) & 15u) != 0u));
     if (p0) {                                        // (p1 only with p0)
       m.st16(S::BRING, q * S::BR + slot0, x0 | (z0 << 12) | (kind0 << 14));
       if (p1) m.st16(S::BRING, q * S::BR + slot1, x1 | (ASK << 14));
@@ -612,7 +613,6 @@ struct EvLane {
       const uint32_t j = pin ? ctz32(in_mask) : 0u;
       const uint32_t q = j / (uint32_t)(N + 1);
       const uint32_t r = j - q * (uint32_t)(N + 1);
-      const bool tick = pin && r == 0u;
       const bool resp = pin && r != 0u;
       const uint32_t ra = r - 1u;
       const uint32_t Lr = q * (uint32_t)N + (resp ? ra : 0u);
@@ -636,24 +636,28 @@ struct EvLane {
       uint32_t k0o = NONE, x0o = 0, z0o = 0;
       bool b1 = false;                                // the restart's AskForTicket (Client.hs:185)
       const uint32_t maj = (uint32_t)N >> 1;          // haveMajority: acks > floor(N/2), :191-194
+      // the input's kind (response kinds 0-2, 3 = Tick, 4 = none) with the state, as one key
+      const uint32_t key = (pin ? (r == 0u ? 3u : rkind) : 4u) * 4u + R;
       // handleTick, Client.hs:196-207
-      const bool t_go = tick && R == IDLE;
-      // HaveTicket, :128-140
-      const bool h_go = resp && rkind == HAVE && R != IDLE && px >= T;
+      const bool t_go = key == 3u * 4u + IDLE;
+      // HaveTicket (state Round1 or Round2), :128-140
+      const bool h_go = key - (HAVE * 4u + ROUND1) < 2u && px >= T;
       // Round1OK, :142-170
-      const bool o_go = resp && rkind == R1OK && R == ROUND1 && T == px;
+      const bool o_go = key == R1OK * 4u + ROUND1 && T == px;
       const uint32_t K1 = K + 1u;
       const bool o_take = MV == 0u || (pz != 0u && !(MT >= py));   // mr <> MostRecent mp (Common.hs:61-65)
       const uint32_t mt = o_take ? py : MT, mv = o_take ? pz : MV;
-      const bool o_maj = o_go && K1 > maj;
+      const bool maj1 = K1 > maj;
+      const bool o_maj = o_go && maj1;
       // Round2Success, :172-189 (no ticket: Q2)
-      const bool s_go = resp && rkind == R2S && R == ROUND2;
-      const bool s_maj = s_go && K1 > maj;
+      const bool s_go = key == R2S * 4u + ROUND2;
+      const bool s_maj = s_go && maj1;
       // the new state
-      const bool restart = t_go || h_go || (s_maj && PD);          // -> Round1 with a new ticket
-      const uint32_t Tn = t_go ? T + 1u : h_go ? px + 1u : (s_maj && PD) ? T + 1u : T;
-      k0o = (t_go || h_go) ? ASK : o_maj ? PROPOSE : s_maj ? EXECUTE : NONE;
-      x0o = (t_go || h_go) ? Tn : o_maj ? px : T;
+      const bool ask = t_go || h_go;
+      const bool restart = ask || (s_maj && PD);                  // -> Round1 with a new ticket
+      const uint32_t Tn = (h_go ? px : T) + (restart ? 1u : 0u);
+      k0o = ask ? ASK : o_maj ? PROPOSE : s_maj ? EXECUTE : NONE;
+      x0o = ask ? Tn : T;                                         // (Propose: px = T)
       const uint32_t C2n = o_maj ? ((mv == 0u) ? CM : mv) : C2;    // Q5: pending whenever mr is Just
       z0o = C2n;
       b1 = s_maj && PD != 0u;

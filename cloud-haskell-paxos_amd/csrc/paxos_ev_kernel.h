@@ -94,8 +94,11 @@ struct EvTotals {
   }
 };
 
+// The compact layout leaves room for 10 resident waves per CU (LDS), i.e. 3
+// on some SIMDs: its register budget is then 168 VGPRs, which the second
+// bound (minimum waves per SIMD) makes the compiler keep to.
 template <int PM, int N, int W, bool CMP>
-__global__ __launch_bounds__(64, 1) void paxos_ev_kernel(EvKParams kp) {
+__global__ __launch_bounds__(64, CMP ? 3 : 1) void paxos_ev_kernel(EvKParams kp) {
   constexpr int POOL = EvPool<PM, N, CMP>::value;
   using S = Shape<PM, N, POOL, W, CMP>;
   __shared__ uint32_t lds[S::WORDS * 64];
