@@ -282,6 +282,13 @@ struct EvLane {
 #endif
   }
 
+  // element q := x for every lane (a lane that keeps its element passes the
+  // old value): the same one-hot masks as get(v, q), which LLVM then shares
+  template <int K>
+  __host__ __device__ static __forceinline__ void put(uint32_t (&v)[K], uint32_t q, uint32_t x) {
+    set_from<K>(v, 1u << q, x);
+  }
+
   // fields of the packed proposer state of p (finish, trace)
   __host__ __device__ uint32_t p_ticket(int p) const { return pw0[p] & 0xFFFu; }
   __host__ __device__ uint32_t p_mr_t(int p) const { return (pw0[p] >> 12) & 0xFFFu; }
@@ -424,10 +431,10 @@ struct EvLane {
   // iterations.  Payloads go to the next ring slots of q.
   __host__ __device__ __forceinline__ void broadcast(uint32_t q, uint32_t kind0, uint32_t x0, uint32_t z0, bool p0,
                                                      uint32_t x1, bool p1, uint32_t val) {
-    rounds += ((p0 && kind0 == ASK) ? 1u : 0u) + (p1 ? 1u : 0u);
-    const bool ex = p0 && kind0 == EXECUTE;
+    rounds += ((p0 & (kind0 == ASK)) ? 1u : 0u) + (p1 ? 1u : 0u);
+    const bool ex = p0 & (kind0 == EXECUTE);
     execs += ex ? 1u : 0u;
-    const bool first = ex && dval == 0u;             // the decided value: first Execute (Client.hs:178)
+    const bool first = ex & (dval == 0u);             // the decided value: first Execute (Client.hs:178)
     dval = first ? val : dval;
     dtick = first ? x0 : dtick;
     const uint32_t slot0 = get(bnext, q), slot1 = (slot0 + 1u) & (S::BR - 1u);
@@ -441,7 +448,7 @@ struct EvLane {
     }
     pq |= (p0 ? ((q << 3) | slot0) << (5u * pq_len) : 0u) | (p1 ? ((q << 3) | slot1) << (5u * pq_len + 5u) : 0u);
     pq_len += (p0 ? 1u : 0u) + (p1 ? 1u : 0u);
-    set(bnext, q, (slot0 + (p0 ? 1u : 0u) + (p1 ? 1u : 0u)) & (S::BR - 1u), p0);
+    put(bnext, q, (slot0 + (p0 ? 1u : 0u) + (p1 ? 1u : 0u)) & (S::BR - 1u));
   }
 
   // the next copy of the oldest pending broadcast, on link cp -> ca (Philox
@@ -451,44 +458,44 @@ struct EvLane {
     // the broadcast's own step: s, or s - 1 for one carried over by end_op
     const uint32_t sb = (uint32_t)s - (pq_old ? 1u : 0u);
     const uint32_t s4 = sb & 15u;
-    const bool snd = act && pq_len != 0u;
+    const bool snd = act & (pq_len != 0u);
     const uint32_t ce = pq & 31u;
     const uint32_t cp = ce >> 3, cslot = ce & 7u, ca = acur;
     const uint32_t ck = get(nsent, cp);
     {                                                // (branch-free: selects, no exec-mask branches)
       const uint32_t a1 = acur + 1u;
-      const bool wrap = snd && a1 == (uint32_t)N;    // the broadcast's last copy
+      const bool wrap = snd & (a1 == (uint32_t)N);    // the broadcast's last copy
       acur = wrap ? 0u : (snd ? a1 : acur);
       pq = wrap ? pq >> 5 : pq;
       pq_len -= wrap ? 1u : 0u;
-      pq_old = pq_old && !wrap;
-      set(nsent, cp, ck + 1u, wrap);
+      pq_old = pq_old & !wrap;
+      put(nsent, cp, ck + (wrap ? 1u : 0u));
     }
     // the draw is computed unconditionally (a branch around it would keep
     // the iteration's three independent Philox chains from interleaving)
     const uint4 w = draw(ck, (1u << 24) | (cp << 8) | ca, kp);
-    const bool ok = !(lossy && w.x <= loss_m1);
+    const bool ok = !(lossy & (w.x <= loss_m1));
     const uint32_t d = 1u + mulhi_n(w.y, dmax);      // (delay_max <= 1: always 1)
     msgs += snd ? 1u : 0u;
     // enqueue (predicated: inactive lanes store to the dummy word)
-    const bool go = snd && ok;
+    const bool go = snd & ok;
     const uint32_t Lq = ca * (uint32_t)PM + cp;
     const uint32_t wq = m.ld(S::REQ + Lq);
     const uint32_t qlen = (wq >> S::QL) & QLM;
-    bailed = bailed || (go && qlen >= (uint32_t)S::QC);
+    bailed = bailed | (go & (qlen >= (uint32_t)S::QC));
     const uint32_t rel = (((wq >> ((7u * qlen - 4u) & 31u)) & 15u) - s4) & (qlen ? 15u : 0u);   // tail's due - sb
     const uint32_t due_rel = d > rel ? d : rel;
     const uint32_t ent = cslot | (((s4 + due_rel) & 15u) << 3);
     // (inactive lanes store their word back unchanged)
     m.st(S::REQ + Lq, go ? (wq & ~(QLM << S::QL)) | (ent << (7u * qlen)) | ((qlen + 1u) << S::QL) : wq);
-    set(refc, cp, get(refc, cp) + (1u << (4u * cslot)), go);
+    put(refc, cp, get(refc, cp) + (go ? 1u << (4u * cslot) : 0u));
     // due at s (a carried-over copy with the shortest delay): straight into
     // this step's due links, else into the wheel
-    const bool now = EARLY && sb + due_rel == (uint32_t)s;
+    const bool now = EARLY & (sb + due_rel == (uint32_t)s);
     const uint32_t slot = (sb + due_rel) & WM;
-    m.orw(S::WHEEL + slot * S::WW, (go && !now) ? 1u << Lq : 0u);
-    occ |= (go && !now) ? (1u << slot) : 0u;
-    acc_mask |= (go && now) ? (1u << Lq) : 0u;
+    m.orw(S::WHEEL + slot * S::WW, (go & !now) ? 1u << Lq : 0u);
+    occ |= (go & !now) ? (1u << slot) : 0u;
+    acc_mask |= (go & now) ? (1u << Lq) : 0u;
     in_flight += go ? 1u : 0u;
   }
 
@@ -513,8 +520,8 @@ struct EvLane {
     // while a carried-over broadcast has copies left, only the acceptors it
     // has reached may run (its copy to acceptor a may be due now, and a takes
     // its requests in (p, seq) order)
-    const uint32_t ready = (EARLY && pq_old) ? acc_mask & ((1u << (acur * (uint32_t)PM)) - 1u) : acc_mask;
-    const bool acc = act && ready != 0u;
+    const uint32_t ready = (EARLY & pq_old) ? acc_mask & ((1u << (acur * (uint32_t)PM)) - 1u) : acc_mask;
+    const bool acc = act & (ready != 0u);
     const uint32_t L = acc ? ctz32(ready) : 0u;
     const uint32_t a = L / (uint32_t)PM, p = L - a * (uint32_t)PM;
     const uint32_t wq = m.ld(S::REQ + L);
@@ -522,27 +529,27 @@ struct EvLane {
     const uint32_t len = (wq >> S::QL) & QLM;
     const uint32_t bslot = wq & 7u;
     const uint32_t rq2 = ((wq & ((1u << S::QL) - 1u)) >> 7) | ((len - 1u) << S::QL);
-    const bool keep = len > 1u && ((rq2 >> 3) & 15u) == s4;
-    acc_mask = (acc && !keep) ? (acc_mask & ~(1u << L)) : acc_mask;
+    const bool keep = (len > 1u) & (((rq2 >> 3) & 15u) == s4);
+    acc_mask = (acc & !keep) ? (acc_mask & ~(1u << L)) : acc_mask;
     in_flight -= acc ? 1u : 0u;
     const uint32_t w16 = m.ld16(S::BRING, p * S::BR + bslot);
-    set(refc, p, get(refc, p) - (1u << (4u * bslot)), acc);
+    put(refc, p, get(refc, p) - (acc ? 1u << (4u * bslot) : 0u));
     const uint32_t kind = w16 >> 14, x = w16 & 0xFFFu, z = (w16 >> 12) & 3u;
     const uint32_t A = get(accw, a);
     const bool dead = ((A >> 26) & 1u) != 0u;
     const uint32_t wa = get(win, a);                 // isolated at s: c0 <= s < c1 (SEMANTICS §4)
-    const bool isol = (wa & 0xFFFFu) <= (uint32_t)s && (uint32_t)s < (wa >> 16);
-    const bool live = acc && !dead && !isol;
+    const bool isol = ((wa & 0xFFFFu) <= (uint32_t)s) & ((uint32_t)s < (wa >> 16));
+    const bool live = acc & !dead & !isol;
     const uint32_t rb = (kind == PROPOSE) ? 12u : 8u;
     canon += acc ? (live ? 2u * rb + 32u : rb) : 0u;
     const uint32_t t_max = A & 0xFFFu, t_store = (A >> 12) & 0xFFFu, val = (A >> 24) & 3u;
     uint32_t log_len = A >> 27;
-    const bool is_ask = live && kind == ASK, is_prop = live && kind == PROPOSE, is_exec = live && kind == EXECUTE;
-    const bool grant = is_ask && !(t_max >= x);                // Server.hs:56
-    const bool accept = is_prop && x == t_max;                 // :66 (equality, not >=)
-    const bool hit = is_exec && t_max == x;                    // :75
-    const bool panic = hit && val == 0u;                       // :76 (Q6)
-    const bool run = hit && val != 0u;                         // :77-78
+    const bool is_ask = live & (kind == ASK), is_prop = live & (kind == PROPOSE), is_exec = live & (kind == EXECUTE);
+    const bool grant = is_ask & !(t_max >= x);                // Server.hs:56
+    const bool accept = is_prop & (x == t_max);                 // :66 (equality, not >=)
+    const bool hit = is_exec & (t_max == x);                    // :75
+    const bool panic = hit & (val == 0u);                       // :76 (Q6)
+    const bool run = hit & (val != 0u);                         // :77-78
     const uint32_t rk = grant ? R1OK : accept ? R2S : HAVE;
     const uint32_t rx = grant ? x : (accept ? 0u : t_max);
     const uint32_t ry = grant ? t_store : 0u;
@@ -553,7 +560,7 @@ struct EvLane {
     lflags |= panic ? (uint32_t)PXB_F_PANIC : 0u;
     if (run) {                                       // executed <>= [c]: log, digest, divergence
       if (log_len >= 31u) bailed = true;
-      set(accd, a, fnv_u32(get(accd, a), (val << 24) | 1u), true);
+      put(accd, a, fnv_u32(get(accd, a), (val << 24) | 1u));
       if (log_len < clog_len) {
         if (((uint32_t)(clog >> (2u * log_len)) & 3u) != val) lflags |= PXB_F_LOG_DIVERGENCE;
       } else {
@@ -562,9 +569,9 @@ struct EvLane {
       }
       log_len += 1u;
     }
-    set(accw, a, nt_max | (nt_store << 12) | (nval << 24) | ((dead || panic) ? (1u << 26) : 0u) | (log_len << 27),
-        live);
-    const bool snd1 = live && !is_exec;              // the reply, on link a -> p
+    // (a lane without a live request rebuilds its old word unchanged)
+    put(accw, a, nt_max | (nt_store << 12) | (nval << 24) | ((dead | panic) ? (1u << 26) : 0u) | (log_len << 27));
+    const bool snd1 = live & !is_exec;              // the reply, on link a -> p
     m.st(S::REQ + L, acc ? rq2 | (S::CMP ? ((kr + (snd1 ? 1u : 0u)) << S::KSH) : 0u) : wq);
 
     // ================= the reply, on a -> p (SEMANTICS §5) =================
@@ -572,18 +579,18 @@ struct EvLane {
     // state dies early; the proposer part only pops due-now heads, so the order
     // of the two on one link does not matter.
     const uint4 w1 = draw(kr, (1u << 24) | (1u << 16) | (p << 8) | a, kp);
-    const bool ok1 = !(lossy && w1.x <= loss_m1);
+    const bool ok1 = !(lossy & (w1.x <= loss_m1));
     const uint32_t d1 = 1u + mulhi_n(w1.y, dmax);
     msgs += snd1 ? 1u : 0u;
-    bailed = bailed || (snd1 && kr == (S::CMP ? (1u << S::KB) - 1u : 0xFFFFu));
+    bailed = bailed | (snd1 & (kr == (S::CMP ? (1u << S::KB) - 1u : 0xFFFFu)));
     if (!S::CMP) m.st16(S::RSEQ, L, snd1 ? kr + 1u : kr);
     {
       // enqueue (predicated: inactive lanes store to the dummy word)
-      const bool go = snd1 && ok1;
+      const bool go = snd1 & ok1;
       const uint32_t Lr = p * (uint32_t)N + a;
       const uint32_t rr = rsp_ld(Lr);
       const uint32_t rlen = (rr >> S::RL) & RLM;
-      bailed = bailed || (go && (rlen >= (uint32_t)S::RC || pfree == 0));
+      bailed = bailed | (go & ((rlen >= (uint32_t)S::RC) | (pfree == 0)));
       const uint32_t rel = (((rr >> S::RD) & 15u) - s4) & (rlen ? 15u : 0u);
       const uint32_t due_rel = d1 > rel ? d1 : rel;
       const uint32_t due4 = (s4 + due_rel) & 15u;
@@ -608,12 +615,12 @@ struct EvLane {
   __host__ __device__ __forceinline__ bool prop_ready() const { return in_mask != 0u && pq_len + 2u <= PQ_CAP; }
   __host__ __device__ __forceinline__ void prop_op(const EvParams& kp, bool act) {
     const uint32_t s4 = (uint32_t)s & 15u;
-    const bool pin = act && in_mask != 0u && pq_len + 2u <= PQ_CAP;
+    const bool pin = act & (in_mask != 0u) & (pq_len + 2u <= PQ_CAP);
     {
       const uint32_t j = pin ? ctz32(in_mask) : 0u;
       const uint32_t q = j / (uint32_t)(N + 1);
       const uint32_t r = j - q * (uint32_t)(N + 1);
-      const bool resp = pin && r != 0u;
+      const bool resp = pin & (r != 0u);
       const uint32_t ra = r - 1u;
       const uint32_t Lr = q * (uint32_t)N + (resp ? ra : 0u);
       const uint32_t rr = rsp_ld(Lr);
@@ -624,8 +631,8 @@ struct EvLane {
       pfree |= resp ? ((pool_mask_t)1 << k) : (pool_mask_t)0;
       m.st(S::RSP + Lr, resp ? ((rr & ((1u << S::RL) - 1u)) >> S::IB) | ((rlen - 1u) << S::RL) | (rr & (15u << S::RD))
                              : rr);
-      const bool rkeep = resp && rlen > 1u && ((pn >> 26) & 15u) == s4;
-      in_mask = (pin && !rkeep) ? (in_mask & ~(1u << j)) : in_mask;
+      const bool rkeep = resp & (rlen > 1u) & (((pn >> 26) & 15u) == s4);
+      in_mask = (pin & !rkeep) ? (in_mask & ~(1u << j)) : in_mask;
       in_flight -= resp ? 1u : 0u;
       const uint32_t rkind = pe >> 30, px = pe & 0xFFFu, py = (pe >> 12) & 0xFFFu, pz = (pe >> 24) & 3u;
       canon += resp ? 2u * (16u >> rkind) : 0u;         // Round1OK 16, HaveTicket 8, Round2Success 4
@@ -641,34 +648,35 @@ struct EvLane {
       // handleTick, Client.hs:196-207
       const bool t_go = key == 3u * 4u + IDLE;
       // HaveTicket (state Round1 or Round2), :128-140
-      const bool h_go = key - (HAVE * 4u + ROUND1) < 2u && px >= T;
+      const bool h_go = (key - (HAVE * 4u + ROUND1) < 2u) & (px >= T);
       // Round1OK, :142-170
-      const bool o_go = key == R1OK * 4u + ROUND1 && T == px;
+      const bool o_go = (key == R1OK * 4u + ROUND1) & (T == px);
       const uint32_t K1 = K + 1u;
-      const bool o_take = MV == 0u || (pz != 0u && !(MT >= py));   // mr <> MostRecent mp (Common.hs:61-65)
+      const bool o_take = (MV == 0u) | ((pz != 0u) & !(MT >= py));   // mr <> MostRecent mp (Common.hs:61-65)
       const uint32_t mt = o_take ? py : MT, mv = o_take ? pz : MV;
       const bool maj1 = K1 > maj;
-      const bool o_maj = o_go && maj1;
+      const bool o_maj = o_go & maj1;
       // Round2Success, :172-189 (no ticket: Q2)
       const bool s_go = key == R2S * 4u + ROUND2;
-      const bool s_maj = s_go && maj1;
+      const bool s_maj = s_go & maj1;
       // the new state
-      const bool ask = t_go || h_go;
-      const bool restart = ask || (s_maj && PD);                  // -> Round1 with a new ticket
+      const bool ask = t_go | h_go;
+      const bool restart = ask | (s_maj & (PD != 0u));                  // -> Round1 with a new ticket
       const uint32_t Tn = (h_go ? px : T) + (restart ? 1u : 0u);
       k0o = ask ? ASK : o_maj ? PROPOSE : s_maj ? EXECUTE : NONE;
       x0o = ask ? Tn : T;                                         // (Propose: px = T)
       const uint32_t C2n = o_maj ? ((mv == 0u) ? CM : mv) : C2;    // Q5: pending whenever mr is Just
       z0o = C2n;
-      b1 = s_maj && PD != 0u;
+      b1 = s_maj & (PD != 0u);
       const uint32_t Rn = restart ? ROUND1 : o_maj ? ROUND2 : (s_maj ? IDLE : R);
-      const uint32_t Kn = (restart || o_maj || s_maj) ? 0u : ((o_go || s_go) ? K1 : K);
-      const uint32_t MTn = (restart || o_maj) ? 0u : (o_go ? mt : MT);
-      const uint32_t MVn = (restart || o_maj) ? 0u : (o_go ? mv : MV);
+      const uint32_t Kn = (restart | o_maj | s_maj) ? 0u : ((o_go | s_go) ? K1 : K);
+      const uint32_t MTn = (restart | o_maj) ? 0u : (o_go ? mt : MT);
+      const uint32_t MVn = (restart | o_maj) ? 0u : (o_go ? mv : MV);
       const uint32_t PDn = o_maj ? ((mv != 0u) ? 1u : 0u) : PD;
-      const uint32_t CMn = t_go ? q + 1u : (s_maj && !PD) ? 0u : CM;
-      set(pw0, q, Tn | (MTn << 12) | (Kn << 24) | (Rn << 28) | (PDn << 30), pin);
-      set(pw1, q, MVn | (C2n << 2) | (CMn << 4), pin);
+      const uint32_t CMn = t_go ? q + 1u : (s_maj & (PD == 0u)) ? 0u : CM;
+      // (without an input every field comes out unchanged)
+      put(pw0, q, Tn | (MTn << 12) | (Kn << 24) | (Rn << 28) | (PDn << 30));
+      put(pw1, q, MVn | (C2n << 2) | (CMn << 4));
       broadcast(q, k0o, x0o, z0o, k0o != NONE, Tn, b1, C2n);
     }
   }
@@ -680,21 +688,22 @@ struct EvLane {
   // its own work), which is then the next step whatever else is due.  Their
   // delays are counted from s, so none is due before s + 1.
   __host__ __device__ __forceinline__ bool end_ready(const EvParams& kp) const {
-    return acc_mask == 0u && in_mask == 0u &&
-           (pq_len == 0u || (EARLY && pq_len == 1u && !pq_old && (uint32_t)s + 1u < kp.step_cap));
+    // (non-short-circuit: && / || here became a tree of exec-mask branches)
+    const bool carry = EARLY & (pq_len == 1u) & !pq_old & ((uint32_t)s + 1u < kp.step_cap);
+    return (acc_mask == 0u) & (in_mask == 0u) & ((pq_len == 0u) | carry);
   }
   __host__ __device__ __forceinline__ bool end_op(const EvParams& kp, EvOut& o, bool act) {
     if (act && end_ready(kp)) {
-      const bool quiet = pq_len == 0u && in_flight == 0u && s >= last_tick;
+      const bool quiet = (pq_len == 0u) & (in_flight == 0u) & (s >= last_tick);
       // nothing but lost copies at a carried-over step: the instance was quiet at s - 1
-      const bool back = EARLY && canon == canon0;
+      const bool back = EARLY & (canon == canon0);
       // the next step with a due message or a Tick (skews of absent proposers are 0)
       const uint32_t s1 = (uint32_t)s + 1u;
       const uint32_t rot = ((occ >> (s1 & WM)) | (occ << ((W - (s1 & WM)) & WM))) & ((1u << W) - 1u);
-      uint32_t nx = (occ && pq_len == 0u) ? s1 + ctz32(rot) : (pq_len ? s1 : 0xFFFFu);
+      uint32_t nx = ((occ != 0u) & (pq_len == 0u)) ? s1 + ctz32(rot) : (pq_len ? s1 : 0xFFFFu);
 #pragma unroll
-      for (int q = 0; q < PM; ++q) nx = (skew[q] > (uint32_t)s && skew[q] < nx) ? skew[q] : nx;
-      const bool capped = !quiet && nx >= kp.step_cap;
+      for (int q = 0; q < PM; ++q) nx = ((skew[q] > (uint32_t)s) & (skew[q] < nx)) ? skew[q] : nx;
+      const bool capped = !quiet & (nx >= kp.step_cap);
       if (quiet || capped) {
         s = capped ? (int32_t)kp.step_cap - 1 : (back ? s - 1 : s);
         finish(capped, o);
