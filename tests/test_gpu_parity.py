@@ -241,9 +241,12 @@ def test_device_entry_accumulates_totals(gpu_lib):
 
 def test_work_queue_flush_keeps_totals_exact(gpu_lib):
     """Faulty kernels take instances from a device work queue and flush their
-    packed 16-bit per-slot counts every FLUSH_EVERY (30000) taken instances.
-    With one wave per CU each wave takes ~65K instances here, so every wave
-    flushes mid-run; the totals must still equal the per-instance results."""
+    partial totals mid-run: the general kernel its packed 16-bit per-slot
+    counts every FLUSH_EVERY (30000) taken instances, the per-lane kernel
+    (which this single-decree schedule takes) its per-lane register sums
+    every EV_FLUSH (256) instances of a lane.  With one wave per CU each lane
+    takes ~1K instances here, so every wave flushes mid-run; the totals must
+    still equal the per-instance results."""
     cfg = pxb.Config(seed=0xF1, n_proposers=1, n_acceptors=3, delay_max=2, step_cap=64)
     n = 1 << 24
     os.environ["PXB_BLOCKS_PER_CU"] = "1"
