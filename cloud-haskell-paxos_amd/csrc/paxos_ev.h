@@ -55,7 +55,6 @@
 
 #include "../../include/paxos_batch.h"
 #include "paxos_device.h"
-#include "paxos_ev_sel.h"
 
 namespace pxb {
 namespace ev {
@@ -147,12 +146,6 @@ struct EvOut {
 #ifndef PXB_EV_CPOST
 #define PXB_EV_CPOST 1
 #endif
-#ifndef PXB_EV_SELBLK
-#define PXB_EV_SELBLK 0     // selects as one asm block each (paxos_ev_sel.h)
-#endif
-#ifndef PXB_EV_VKEYS
-#define PXB_EV_VKEYS 1      // Philox round keys precomputed in VGPRs (set_keys)
-#endif
 #ifndef PXB_EV_ACCN
 #define PXB_EV_ACCN 1       // acceptor ops per iteration
 #endif
@@ -170,9 +163,7 @@ struct EvLane {
   static constexpr uint32_t IM = (1u << S::IB) - 1u;
 
   Mem m;
-#if PXB_EV_VKEYS
   uint32_t rk[20];                    // Philox round keys (set_keys): uniform, held in VGPRs
-#endif
   // ---- instance ----
   uint32_t mode;
   uint32_t gid;                       // instance index within the launch
@@ -219,15 +210,6 @@ struct EvLane {
 #endif
     return x;
   }
-  // the Philox key re-read inside the loop: its ten round keys are then two
-  // SALU adds per round, instead of twenty loop-invariant SGPRs that push
-  // the lane predicates into VGPR spill slots
-  __host__ __device__ static __forceinline__ uint32_t skey(uint32_t k) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    __asm__ volatile("" : "+s"(k));
-#endif
-    return k;
-  }
   // Selects by a per-lane index q over a small register array, as bit
   // operations on the one-hot word 1 << q: element i's lane mask is bit i of
   // it sign-extended (one v_bfe_i32), merged with v_bfi_b32.  A compare per
@@ -260,11 +242,7 @@ struct EvLane {
   }
   template <int K>
   __host__ __device__ static __forceinline__ uint32_t get(const uint32_t (&v)[K], uint32_t q) {
-#if defined(__HIP_DEVICE_COMPILE__) && PXB_EV_SELBLK
-    return Sel<K>::get(v, 1u << q);
-#else
     return get_from<K>(v, 1u << q, v[0]);
-#endif
   }
   template <int K, int I = 0>
   __host__ __device__ static __forceinline__ void set_from(uint32_t (&v)[K], uint32_t oh, uint32_t x) {
@@ -272,14 +250,6 @@ struct EvLane {
       v[I] = bfi(lane_mask<I>(oh), x, v[I]);
       set_from<K, I + 1>(v, oh, x);
     }
-  }
-  template <int K>
-  __host__ __device__ static __forceinline__ void set(uint32_t (&v)[K], uint32_t q, uint32_t x, bool pred) {
-#if defined(__HIP_DEVICE_COMPILE__) && PXB_EV_SELBLK
-    Sel<K>::set(v, pred ? (1u << q) : 0u, x);
-#else
-    set_from<K>(v, pred ? (1u << q) : 0u, x);
-#endif
   }
 
   // element q := x for every lane (a lane that keeps its element passes the
@@ -342,20 +312,14 @@ struct EvLane {
   // the launch's Philox round keys, once per wave: as VGPRs they cost no
   // per-round key arithmetic, and (unlike 20 SGPRs) push nothing into spills
   __host__ __device__ __forceinline__ void set_keys(const EvParams& kp) {
-#if PXB_EV_VKEYS
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
       rk[2 * r] = opaque(kp.k0 + (uint32_t)r * 0x9E3779B9u);
       rk[2 * r + 1] = opaque(kp.k1 + (uint32_t)r * 0xBB67AE85u);
     }
-#endif
   }
-  __host__ __device__ __forceinline__ uint4 draw(uint32_t c2, uint32_t c3, const EvParams& kp) const {
-#if PXB_EV_VKEYS
+  __host__ __device__ __forceinline__ uint4 draw(uint32_t c2, uint32_t c3) const {
     return philox_rk(lo, hi, c2, c3, rk);
-#else
-    return philox(lo, hi, c2, c3, skey(kp.k0), skey(kp.k1));
-#endif
   }
 
   // ---- instance start: parameters, Tick skews, isolation windows (SEMANTICS §4) ----
@@ -473,7 +437,7 @@ struct EvLane {
     }
     // the draw is computed unconditionally (a branch around it would keep
     // the iteration's three independent Philox chains from interleaving)
-    const uint4 w = draw(ck, (1u << 24) | (cp << 8) | ca, kp);
+    const uint4 w = draw(ck, (1u << 24) | (cp << 8) | ca);
     const bool ok = !(lossy & (w.x <= loss_m1));
     const uint32_t d = 1u + mulhi_n(w.y, dmax);      // (delay_max <= 1: always 1)
     msgs += snd ? 1u : 0u;
@@ -578,7 +542,7 @@ struct EvLane {
     // Philox seq = the link's reply count.  Sent before the proposer part so its
     // state dies early; the proposer part only pops due-now heads, so the order
     // of the two on one link does not matter.
-    const uint4 w1 = draw(kr, (1u << 24) | (1u << 16) | (p << 8) | a, kp);
+    const uint4 w1 = draw(kr, (1u << 24) | (1u << 16) | (p << 8) | a);
     const bool ok1 = !(lossy & (w1.x <= loss_m1));
     const uint32_t d1 = 1u + mulhi_n(w1.y, dmax);
     msgs += snd1 ? 1u : 0u;
