@@ -451,7 +451,8 @@ struct EvLane {
     const uint32_t due_rel = d > rel ? d : rel;
     const uint32_t ent = cslot | (((s4 + due_rel) & 15u) << 3);
     // (inactive lanes store their word back unchanged)
-    m.st(S::REQ + Lq, go ? (wq & ~(QLM << S::QL)) | (ent << (7u * qlen)) | ((qlen + 1u) << S::QL) : wq);
+    // (entries above the length are 0: a pop shifts zeros in; a full FIFO bails)
+    m.st(S::REQ + Lq, go ? wq + (1u << S::QL) + (ent << (7u * qlen)) : wq);
     put(refc, cp, get(refc, cp) + (go ? 1u << (4u * cslot) : 0u));
     // due at s (a carried-over copy with the shortest delay): straight into
     // this step's due links, else into the wheel
@@ -492,8 +493,10 @@ struct EvLane {
     const uint32_t kr = S::CMP ? (wq >> S::KSH) : m.ld16(S::RSEQ, L);   // the reply's link sequence number
     const uint32_t len = (wq >> S::QL) & QLM;
     const uint32_t bslot = wq & 7u;
-    const uint32_t rq2 = ((wq & ((1u << S::QL) - 1u)) >> 7) | ((len - 1u) << S::QL);
-    const bool keep = (len > 1u) & (((rq2 >> 3) & 15u) == s4);
+    // the popped word: entries shifted down one, length - 1 (fields above the
+    // entries, length and reply seq, adjusted in place)
+    const uint32_t rq2 = ((wq & ((1u << S::QL) - 1u)) >> 7) + ((wq & ~((1u << S::QL) - 1u)) - (1u << S::QL));
+    const bool keep = (len > 1u) & (((wq >> 10) & 15u) == s4);   // the next entry due now too
     acc_mask = (acc & !keep) ? (acc_mask & ~(1u << L)) : acc_mask;
     in_flight -= acc ? 1u : 0u;
     const uint32_t w16 = m.ld16(S::BRING, p * S::BR + bslot);
@@ -536,7 +539,7 @@ struct EvLane {
     // (a lane without a live request rebuilds its old word unchanged)
     put(accw, a, nt_max | (nt_store << 12) | (nval << 24) | ((dead | panic) ? (1u << 26) : 0u) | (log_len << 27));
     const bool snd1 = live & !is_exec;              // the reply, on link a -> p
-    m.st(S::REQ + L, acc ? rq2 | (S::CMP ? ((kr + (snd1 ? 1u : 0u)) << S::KSH) : 0u) : wq);
+    m.st(S::REQ + L, acc ? rq2 + ((S::CMP && snd1) ? 1u << S::KSH : 0u) : wq);
 
     // ================= the reply, on a -> p (SEMANTICS §5) =================
     // Philox seq = the link's reply count.  Sent before the proposer part so its
@@ -564,9 +567,8 @@ struct EvLane {
       // free, to the link word, which the next store writes back unchanged
       m.st(pfree ? S::POOLW + k2 : S::RSP + Lr, rx | (ry << 12) | (rz << 24) | (due4 << 26) | (rk << 30));
       pfree &= go ? ~((pool_mask_t)1 << k2) : ~(pool_mask_t)0;
-      m.st(S::RSP + Lr, go ? (rr & ((1u << (S::IB * rlen)) - 1u)) | (k2 << (S::IB * rlen)) | ((rlen + 1u) << S::RL) |
-                                 (due4 << S::RD)
-                           : rr);
+      // (entries above the length are 0, as for the request FIFOs)
+      m.st(S::RSP + Lr, go ? ((rr + (1u << S::RL) + (k2 << (S::IB * rlen))) & ~(15u << S::RD)) | (due4 << S::RD) : rr);
       const uint32_t slot = ((uint32_t)s + due_rel) & WM;
       m.orw(S::WHEEL + slot * S::WW + (S::WW == 2 ? 1u : 0u), go ? 1u << (S::ISH + p * (N + 1) + 1u + a) : 0u);
       occ |= go ? (1u << slot) : 0u;
@@ -593,8 +595,8 @@ struct EvLane {
       const uint32_t pe = m.ld(S::POOLW + k);
       const uint32_t pn = m.ld(S::POOLW + ((rr >> S::IB) & IM));
       pfree |= resp ? ((pool_mask_t)1 << k) : (pool_mask_t)0;
-      m.st(S::RSP + Lr, resp ? ((rr & ((1u << S::RL) - 1u)) >> S::IB) | ((rlen - 1u) << S::RL) | (rr & (15u << S::RD))
-                             : rr);
+      m.st(S::RSP + Lr, resp ? ((rr & ((1u << S::RL) - 1u)) >> S::IB) + ((rr & ~((1u << S::RL) - 1u)) - (1u << S::RL))
+                             : rr);                         // (popped: entries down one, length - 1)
       const bool rkeep = resp & (rlen > 1u) & (((pn >> 26) & 15u) == s4);
       in_mask = (pin & !rkeep) ? (in_mask & ~(1u << j)) : in_mask;
       in_flight -= resp ? 1u : 0u;
