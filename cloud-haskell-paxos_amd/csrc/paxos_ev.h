@@ -525,7 +525,7 @@ struct EvLane {
     const uint32_t nt_store = accept ? x : (run ? 0u : t_store);
     const uint32_t nval = accept ? z : (run ? 0u : val);
     lflags |= panic ? (uint32_t)PXB_F_PANIC : 0u;
-    if (run) {                                       // executed <>= [c]: log, digest, divergence
+    if (__builtin_expect(run, 0)) {                  // executed <>= [c]: log, digest, divergence
       if (log_len >= 31u) bailed = true;
       put(accd, a, fnv_u32(get(accd, a), (val << 24) | 1u));
       if (log_len < clog_len) {
@@ -670,7 +670,7 @@ struct EvLane {
 #pragma unroll
       for (int q = 0; q < PM; ++q) nx = ((skew[q] > (uint32_t)s) & (skew[q] < nx)) ? skew[q] : nx;
       const bool capped = !quiet & (nx >= kp.step_cap);
-      if (quiet || capped) {
+      if (__builtin_expect(quiet | capped, 0)) {
         s = capped ? (int32_t)kp.step_cap - 1 : (back ? s - 1 : s);
         finish(capped, o);
         return true;

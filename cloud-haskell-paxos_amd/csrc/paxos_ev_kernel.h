@@ -145,12 +145,12 @@ __global__ __launch_bounds__(64, CMP ? 3 : 1) void paxos_ev_kernel(EvKParams kp)
     if (L.mode != M_IDLE) {
       EvOut o;
       const bool done = L.step(kp.p, o);
-      if (L.bailed) {                         // beyond this kernel's capacities: re-run by the general kernel
+      if (__builtin_expect(L.bailed, 0)) {    // beyond this kernel's capacities: re-run by the general kernel
         const uint32_t pos = atomicAdd(kp.bail_n, 1u);
         if (pos < kp.bail_cap) kp.bail_ids[pos] = L.gid;
         L.mode = M_IDLE;
         L.bailed = false;
-      } else if (done) {
+      } else if (__builtin_expect(done, 0)) {
         const uint32_t f = o.flags;
         tot.c[0] += 1u;
         tot.c[1] += (f & PXB_F_UNDECIDED) ? 1u : 0u;
