@@ -140,16 +140,6 @@ struct EvOut {
   uint32_t steps;
 };
 
-#ifndef PXB_EV_CPRE
-#define PXB_EV_CPRE 1
-#endif
-#ifndef PXB_EV_CPOST
-#define PXB_EV_CPOST 1
-#endif
-#ifndef PXB_EV_ACCN
-#define PXB_EV_ACCN 1       // acceptor ops per iteration
-#endif
-
 // EARLY: a step may end with the copies of its last broadcast still to send
 // (see end_op); the trace kernel turns it off so that its per-step records
 // hold every message of the step in flight, as the oracle's do.
@@ -418,7 +408,13 @@ struct EvLane {
   // the next copy of the oldest pending broadcast, on link cp -> ca (Philox
   // seq = the broadcast index, the link's seq: every broadcast tries every acceptor)
   __host__ __device__ __forceinline__ bool copy_ready() const { return pq_len != 0u; }
-  __host__ __device__ __forceinline__ void copy_send(const EvParams& kp, bool act) {
+  // the Philox counter words of the next copy (seq = the broadcast's index on
+  // its proposer, tag = (proposer, acceptor))
+  __host__ __device__ __forceinline__ uint2 copy_ctr() const {
+    const uint32_t cp = (pq & 31u) >> 3;
+    return make_uint2(get(nsent, cp), (1u << 24) | (cp << 8) | acur);
+  }
+  __host__ __device__ __forceinline__ void copy_send(const EvParams& kp, bool act, const uint4& w) {
     // the broadcast's own step: s, or s - 1 for one carried over by end_op
     const uint32_t sb = (uint32_t)s - (pq_old ? 1u : 0u);
     const uint32_t s4 = sb & 15u;
@@ -435,9 +431,7 @@ struct EvLane {
       pq_old = pq_old & !wrap;
       put(nsent, cp, ck + (wrap ? 1u : 0u));
     }
-    // the draw is computed unconditionally (a branch around it would keep
-    // the iteration's three independent Philox chains from interleaving)
-    const uint4 w = draw(ck, (1u << 24) | (cp << 8) | ca);
+    // (w: the draw of copy_ctr() taken before this call)
     const bool ok = !(lossy & (w.x <= loss_m1));
     const uint32_t d = 1u + mulhi_n(w.y, dmax);      // (delay_max <= 1: always 1)
     msgs += snd ? 1u : 0u;
@@ -464,15 +458,19 @@ struct EvLane {
     in_flight += go ? 1u : 0u;
   }
 
-  // one iteration of all four parts; returns true when the instance ended (outputs in o)
+  // One iteration: the acceptor part, a copy (when the acceptor sent no
+  // reply), the proposer part, a copy, the step end; returns true when the
+  // instance ended (outputs in o).  Two Philox draws per iteration: the
+  // first serves the reply, or else the first copy (1.4 of the 3 sends an
+  // iteration can make are used on average; the first copy's counter is
+  // known before the acceptor part, which does not touch the pending queue).
   __host__ __device__ __forceinline__ bool step(const EvParams& kp, EvOut& o) {
-#pragma unroll
-    for (int c = 0; c < PXB_EV_ACCN; ++c) acc_op(kp, true);
-#pragma unroll
-    for (int c = 0; c < PXB_EV_CPRE; ++c) copy_send(kp, true);
+    bool replied;
+    const uint4 w0 = acc_op(kp, true, copy_ctr(), replied);
+    copy_send(kp, !replied, w0);
     prop_op(kp, true);
-#pragma unroll
-    for (int c = 0; c < PXB_EV_CPOST; ++c) copy_send(kp, true);
+    const uint2 c = copy_ctr();
+    copy_send(kp, true, draw(c.x, c.y));
     return end_op(kp, o, true);
   }
 
@@ -480,7 +478,7 @@ struct EvLane {
   __host__ __device__ __forceinline__ bool acc_ready() const {
     return ((EARLY && pq_old) ? acc_mask & ((1u << (acur * (uint32_t)PM)) - 1u) : acc_mask) != 0u;
   }
-  __host__ __device__ __forceinline__ void acc_op(const EvParams& kp, bool act) {
+  __host__ __device__ __forceinline__ uint4 acc_op(const EvParams& kp, bool act, uint2 cc, bool& replied) {
     const uint32_t s4 = (uint32_t)s & 15u;
     // while a carried-over broadcast has copies left, only the acceptors it
     // has reached may run (its copy to acceptor a may be due now, and a takes
@@ -545,7 +543,9 @@ struct EvLane {
     // Philox seq = the link's reply count.  Sent before the proposer part so its
     // state dies early; the proposer part only pops due-now heads, so the order
     // of the two on one link does not matter.
-    const uint4 w1 = draw(kr, (1u << 24) | (1u << 16) | (p << 8) | a);
+    // (one draw: this reply's, or, without one, the next copy's: cc)
+    const uint4 w1 = draw(snd1 ? kr : cc.x, snd1 ? (1u << 24) | (1u << 16) | (p << 8) | a : cc.y);
+    replied = snd1;
     const bool ok1 = !(lossy & (w1.x <= loss_m1));
     const uint32_t d1 = 1u + mulhi_n(w1.y, dmax);
     msgs += snd1 ? 1u : 0u;
@@ -574,7 +574,7 @@ struct EvLane {
       occ |= go ? (1u << slot) : 0u;
       in_flight += go ? 1u : 0u;
     }
-
+    return w1;
   }
 
   // ================= PROP: one input of one proposer =================
