@@ -408,6 +408,69 @@ struct EvLane {
   // the next copy of the oldest pending broadcast, on link cp -> ca (Philox
   // seq = the broadcast index, the link's seq: every broadcast tries every acceptor)
   __host__ __device__ __forceinline__ bool copy_ready() const { return pq_len != 0u; }
+  // the acceptor's reply, handed to send_first: link, pool word (without its
+  // due), proposer-input bit
+  struct Reply {
+    bool snd;
+    uint32_t Lr, pw, bit;
+  };
+
+  // The iteration's first send, on draw w: the acceptor's reply on link
+  // a -> p (response FIFO + pool word) when there is one, else the next copy
+  // of the oldest pending broadcast (request FIFO); one code path for both.
+  __host__ __device__ __forceinline__ void send_first(const EvParams& kp, const uint4& w, const Reply& rp) {
+    const bool isR = rp.snd;
+    // the copy's bookkeeping (as in copy_send)
+    const uint32_t sb = (uint32_t)s - (pq_old ? 1u : 0u);
+    const bool csnd = !isR & (pq_len != 0u);
+    const uint32_t ce = pq & 31u;
+    const uint32_t cp = ce >> 3, cslot = ce & 7u, ca = acur;
+    const uint32_t ck = get(nsent, cp);
+    {
+      const uint32_t a1 = acur + 1u;
+      const bool wrap = csnd & (a1 == (uint32_t)N);
+      acur = wrap ? 0u : (csnd ? a1 : acur);
+      pq = wrap ? pq >> 5 : pq;
+      pq_len -= wrap ? 1u : 0u;
+      pq_old = pq_old & !wrap;
+      put(nsent, cp, ck + (wrap ? 1u : 0u));
+    }
+    msgs += csnd ? 1u : 0u;                          // (the reply counted itself)
+    const bool snd = isR | csnd;
+    const bool ok = !(lossy & (w.x <= loss_m1));
+    const uint32_t d = 1u + mulhi_n(w.y, dmax);
+    const bool go = snd & ok;
+    const uint32_t base = isR ? (uint32_t)s : sb;   // the send step (a carried copy's is s - 1)
+    const uint32_t b4 = base & 15u;
+    const uint32_t Lq = ca * (uint32_t)PM + cp;
+    const uint32_t lw = isR ? S::RSP + rp.Lr : S::REQ + Lq;   // the link word
+    const uint32_t wv = m.ld(lw);
+    const uint32_t len = isR ? (wv >> S::RL) & RLM : (wv >> S::QL) & QLM;
+    const uint32_t tail = isR ? (wv >> S::RD) & 15u : (wv >> ((7u * len - 4u) & 31u)) & 15u;
+    const uint32_t rel = (tail - b4) & (len ? 15u : 0u);
+    const uint32_t due_rel = d > rel ? d : rel;
+    const uint32_t due4 = (b4 + due_rel) & 15u;
+    bailed = bailed | (go & (isR ? (len >= (uint32_t)S::RC) | (pfree == 0) : (len >= (uint32_t)S::QC)));
+    const uint32_t k2 = (POOL > 32) ? (uint32_t)__builtin_ctzll((unsigned long long)pfree | (1ull << 63))
+                                    : ctz32((uint32_t)pfree) & 31u;
+    // the pool word: to a free entry (harmless unless a reply goes), or, with
+    // none free, to the link word, which the next store rewrites
+    m.st(pfree ? S::POOLW + k2 : lw, rp.pw | (due4 << 26));
+    pfree &= (go & isR) ? ~((pool_mask_t)1 << k2) : ~(pool_mask_t)0;
+    // (entries above a FIFO's length are 0: appends are additions)
+    const uint32_t nR = ((wv + (1u << S::RL) + (k2 << (S::IB * len))) & ~(15u << S::RD)) | (due4 << S::RD);
+    const uint32_t nQ = wv + (1u << S::QL) + ((cslot | (due4 << 3)) << (7u * len));
+    m.st(lw, go ? (isR ? nR : nQ) : wv);
+    put(refc, cp, get(refc, cp) + ((go & !isR) ? 1u << (4u * cslot) : 0u));
+    // a carried copy due now joins this step's due links, the rest the wheel
+    const bool now = EARLY & !isR & (base + due_rel == (uint32_t)s);
+    const uint32_t slot = (base + due_rel) & WM;
+    m.orw(S::WHEEL + slot * S::WW + ((S::WW == 2 && isR) ? 1u : 0u), (go & !now) ? 1u << (isR ? rp.bit : Lq) : 0u);
+    occ |= (go & !now) ? (1u << slot) : 0u;
+    acc_mask |= (go & now) ? (1u << Lq) : 0u;
+    in_flight += go ? 1u : 0u;
+  }
+
   // the Philox counter words of the next copy (seq = the broadcast's index on
   // its proposer, tag = (proposer, acceptor))
   __host__ __device__ __forceinline__ uint2 copy_ctr() const {
@@ -465,9 +528,9 @@ struct EvLane {
   // iteration can make are used on average; the first copy's counter is
   // known before the acceptor part, which does not touch the pending queue).
   __host__ __device__ __forceinline__ bool step(const EvParams& kp, EvOut& o) {
-    bool replied;
-    const uint4 w0 = acc_op(kp, true, copy_ctr(), replied);
-    copy_send(kp, !replied, w0);
+    Reply rp;
+    const uint4 w0 = acc_op(kp, true, copy_ctr(), rp);
+    send_first(kp, w0, rp);
     prop_op(kp, true);
     const uint2 c = copy_ctr();
     copy_send(kp, true, draw(c.x, c.y));
@@ -478,7 +541,7 @@ struct EvLane {
   __host__ __device__ __forceinline__ bool acc_ready() const {
     return ((EARLY && pq_old) ? acc_mask & ((1u << (acur * (uint32_t)PM)) - 1u) : acc_mask) != 0u;
   }
-  __host__ __device__ __forceinline__ uint4 acc_op(const EvParams& kp, bool act, uint2 cc, bool& replied) {
+  __host__ __device__ __forceinline__ uint4 acc_op(const EvParams& kp, bool act, uint2 cc, Reply& rp) {
     const uint32_t s4 = (uint32_t)s & 15u;
     // while a carried-over broadcast has copies left, only the acceptors it
     // has reached may run (its copy to acceptor a may be due now, and a takes
@@ -545,35 +608,13 @@ struct EvLane {
     // of the two on one link does not matter.
     // (one draw: this reply's, or, without one, the next copy's: cc)
     const uint4 w1 = draw(snd1 ? kr : cc.x, snd1 ? (1u << 24) | (1u << 16) | (p << 8) | a : cc.y);
-    replied = snd1;
-    const bool ok1 = !(lossy & (w1.x <= loss_m1));
-    const uint32_t d1 = 1u + mulhi_n(w1.y, dmax);
     msgs += snd1 ? 1u : 0u;
     bailed = bailed | (snd1 & (kr == (S::CMP ? (1u << S::KB) - 1u : 0xFFFFu)));
     if (!S::CMP) m.st16(S::RSEQ, L, snd1 ? kr + 1u : kr);
-    {
-      // enqueue (predicated: inactive lanes store to the dummy word)
-      const bool go = snd1 & ok1;
-      const uint32_t Lr = p * (uint32_t)N + a;
-      const uint32_t rr = rsp_ld(Lr);
-      const uint32_t rlen = (rr >> S::RL) & RLM;
-      bailed = bailed | (go & ((rlen >= (uint32_t)S::RC) | (pfree == 0)));
-      const uint32_t rel = (((rr >> S::RD) & 15u) - s4) & (rlen ? 15u : 0u);
-      const uint32_t due_rel = d1 > rel ? d1 : rel;
-      const uint32_t due4 = (s4 + due_rel) & 15u;
-      const uint32_t k2 = (POOL > 32) ? (uint32_t)__builtin_ctzll((unsigned long long)pfree | (1ull << 63))
-                                      : ctz32((uint32_t)pfree) & 31u;
-      // inactive lanes: the pool word goes to a free entry, or, with none
-      // free, to the link word, which the next store writes back unchanged
-      m.st(pfree ? S::POOLW + k2 : S::RSP + Lr, rx | (ry << 12) | (rz << 24) | (due4 << 26) | (rk << 30));
-      pfree &= go ? ~((pool_mask_t)1 << k2) : ~(pool_mask_t)0;
-      // (entries above the length are 0, as for the request FIFOs)
-      m.st(S::RSP + Lr, go ? ((rr + (1u << S::RL) + (k2 << (S::IB * rlen))) & ~(15u << S::RD)) | (due4 << S::RD) : rr);
-      const uint32_t slot = ((uint32_t)s + due_rel) & WM;
-      m.orw(S::WHEEL + slot * S::WW + (S::WW == 2 ? 1u : 0u), go ? 1u << (S::ISH + p * (N + 1) + 1u + a) : 0u);
-      occ |= go ? (1u << slot) : 0u;
-      in_flight += go ? 1u : 0u;
-    }
+    rp.snd = snd1;
+    rp.Lr = p * (uint32_t)N + a;
+    rp.pw = rx | (ry << 12) | (rz << 24) | (rk << 30);
+    rp.bit = S::ISH + p * (N + 1) + 1u + a;
     return w1;
   }
 
