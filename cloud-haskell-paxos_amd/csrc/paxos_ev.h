@@ -325,7 +325,7 @@ struct EvLane {
     loss_m1 = kp.loss_m1;
     uint32_t crash_m1 = kp.crash_m1;
     if (kp.cfg & EV_CFG_RANDOMIZE) {                  // config-5 fuzz (SEMANTICS §4)
-      const uint4 w = philox(lo, hi, 0u, 4u << 24, kp.k0, kp.k1);
+      const uint4 w = draw(0u, 4u << 24);
       P = 1u + mulhi_n(w.x, kp.n_prop);
       const uint64_t lt = ev_threshold(mulhi_n(w.y, kp.loss_ppm + 1u));
       dmax = 1u + mulhi_n(w.z, kp.delay_max);
@@ -336,7 +336,7 @@ struct EvLane {
       crash_m1 = (uint32_t)(ct - 1ull);
     }
     uint4 wsk = make_uint4(0, 0, 0, 0);
-    if (kp.skew_max > 0u) wsk = philox(lo, hi, 0u, 2u << 24, kp.k0, kp.k1);
+    if (kp.skew_max > 0u) wsk = draw(0u, 2u << 24);
     last_tick = 0;
 #pragma unroll
     for (int p = 0; p < PM; ++p) {
@@ -350,7 +350,7 @@ struct EvLane {
     for (int a = 0; a < N; ++a) {
       uint32_t c0 = 0, c1 = 0;
       if (crashy) {
-        const uint4 w = philox(lo, hi, 0u, (3u << 24) | (uint32_t)a, kp.k0, kp.k1);
+        const uint4 w = draw(0u, (3u << 24) | (uint32_t)a);
         if (w.x <= crash_m1) {
           c0 = mulhi_n(w.y, kp.crash_start_max + 1u);
           c1 = c0 + 1u + mulhi_n(w.z, kp.crash_len_max);
