@@ -206,7 +206,12 @@ static uint32_t g_qseq[64];
 constexpr uint64_t EV_CHUNK = 1ull << 24;
 constexpr int EV_MIN_BLOCKS = 6;
 constexpr uint32_t EV_BAIL_CAP = 1u << 20;
+// split routing (fuzzed P = 3 batches, config 5): the per-lane kernel of a
+// two-proposer shape takes the instances that drew P <= 2 and lists the P = 3
+// ones (a third) with its bails, so their list holds half a chunk
+constexpr uint32_t EV_SPLIT_BAIL_CAP = (uint32_t)(EV_CHUNK / 2);
 static uint32_t* g_bail[64][QSLOTS];
+static uint32_t g_bail_cap[64][QSLOTS];
 static int g_eocc[3][4][10][64];
 
 static int hip_fail(hipError_t e) {
@@ -320,6 +325,7 @@ int pxb_shutdown(void) {
       for (int k = 0; k < QSLOTS; ++k) {
         if (g_bail[d][k]) (void)hipFree(g_bail[d][k]);
         g_bail[d][k] = nullptr;
+        g_bail_cap[d][k] = 0;
       }
       g_qseq[d] = 0;
     }
@@ -369,13 +375,19 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
   bool use_ev = !ff && !logm && ev::eligible(cfg) && !(no_ev && atoi(no_ev) > 0);
   // tests: a smaller bailed-id list, to exercise its overflow path
   const char* cap_s = getenv("PXB_EV_BAIL_CAP");
-  const uint32_t bail_cap = (cap_s && atoi(cap_s) >= 0) ? std::min<uint32_t>((uint32_t)atoi(cap_s), EV_BAIL_CAP)
-                                                      : EV_BAIL_CAP;
   kernel_fn fn = pick(cfg->n_proposers, cfg->n_acceptors, logm, ff);
   if (!fn) return PXB_E_INVAL;
   const int layout = ev::layout_for(cfg);
-  const ev_kernel_ptr efn = use_ev ? ev_pick(cfg->n_proposers, cfg->n_acceptors, layout) : nullptr;
+  ev_kernel_ptr efn = use_ev ? ev_pick(cfg->n_proposers, cfg->n_acceptors, layout) : nullptr;
   if (use_ev && !efn) return PXB_E_INVAL;
+  // fuzzed three-proposer batches whose per-lane layout fits too few waves:
+  // the two-proposer shape runs the instances that drew P <= 2, the general
+  // kernel the rest (PXB_NO_SPLIT=1 turns this off)
+  const char* no_split = getenv("PXB_NO_SPLIT");
+  const bool may_split = use_ev && (cfg->flags & PXB_CFG_RANDOMIZE) && cfg->n_proposers == 3 &&
+                         !(no_split && atoi(no_split) > 0);
+  bool split = false;
+  uint32_t bail_cap = EV_BAIL_CAP;
   const hipStream_t st = (hipStream_t)stream;
   int occ, cus, eocc = 0;
   {
@@ -405,8 +417,25 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
         eo = std::max(1, nb);
       }
       eocc = eo;
-      if (eocc < EV_MIN_BLOCKS && !(force_ev && atoi(force_ev) > 0)) use_ev = false;
+      const bool forced = force_ev && atoi(force_ev) > 0;
+      if (eocc < EV_MIN_BLOCKS && may_split && !forced) {
+        int& so = g_eocc[layout][2][cfg->n_acceptors][dev];
+        const ev_kernel_ptr sfn = ev_pick(2, cfg->n_acceptors, layout);
+        if (sfn && !so) {
+          int nb = 0;
+          HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)sfn, 64, 0));
+          so = std::max(1, nb);
+        }
+        if (sfn && so >= EV_MIN_BLOCKS) {
+          split = true;
+          efn = sfn;
+          eocc = so;
+          bail_cap = EV_SPLIT_BAIL_CAP;
+        }
+      }
+      if (eocc < EV_MIN_BLOCKS && !forced) use_ev = false;
     }
+    if (cap_s && atoi(cap_s) >= 0) bail_cap = std::min<uint32_t>((uint32_t)atoi(cap_s), bail_cap);
     if (int rc2 = ensure_slots(dev)) return rc2;
     const char* cap_env = getenv("PXB_BLOCKS_PER_CU");   // tests / experiments: cap residency
     if (cap_env && atoi(cap_env) > 0) {
@@ -474,7 +503,18 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
       kp.part = slot;
       kp.queue = reinterpret_cast<uint32_t*>(slot + 2 * ROWS_U64);
       if (use_ev) {
-        if (!g_bail[dev][sidx]) HIPCHK(hipMalloc(&g_bail[dev][sidx], (size_t)EV_BAIL_CAP * sizeof(uint32_t)));
+        const uint32_t need = split ? EV_SPLIT_BAIL_CAP : EV_BAIL_CAP;
+        if (g_bail_cap[dev][sidx] < need) {
+          // (the slot's previous launches on any stream may still read the old list)
+          if (g_bail[dev][sidx]) {
+            HIPCHK(hipDeviceSynchronize());
+            HIPCHK(hipFree(g_bail[dev][sidx]));
+            g_bail[dev][sidx] = nullptr;
+            g_bail_cap[dev][sidx] = 0;
+          }
+          HIPCHK(hipMalloc(&g_bail[dev][sidx], (size_t)need * sizeof(uint32_t)));
+          g_bail_cap[dev][sidx] = need;
+        }
         bail = g_bail[dev][sidx];
       }
     }

@@ -374,7 +374,9 @@ struct EvLane {
     clog = 0ull;
     clog_len = 0u;
     occ = 0u;
-    bailed = false;
+    // a fuzzed instance with more proposers than this shape holds goes to the
+    // general kernel (config 5 runs its P <= 2 instances here: pxb_run_device)
+    bailed = P > (uint32_t)PM;
     mode = M_RUN;
     enter(0);
   }
@@ -785,8 +787,11 @@ __host__ inline EvParams make_params(const pxb_config* c) {
   return p;
 }
 
-// the timing wheel must outlast the longest delay
-__host__ inline int wheel_for(uint32_t delay_max) { return delay_max <= 7 ? 8 : 16; }
+// the timing wheel must outlast the longest delay: sends at step s (or s - 1
+// for a carried-over copy) fall due in [s, s + delay_max] (a link's FIFO tail
+// is at most its last send step + delay_max), the slot of s is emptied on
+// entering s, so 8 slots serve delays up to 8
+__host__ inline int wheel_for(uint32_t delay_max) { return delay_max <= 8 ? 8 : 16; }
 
 // Kernel layout of a launch: 0 = 8-step wheel, 1 = 16-step wheel, 2 = compact
 // links (3-entry request FIFOs sharing a word with the reply seq, a 24-word

@@ -51,7 +51,7 @@ struct EvKParams {
 // schedules with short delays, whose responses in flight stay fewer)
 template <int PM, int N, bool CMP>
 struct EvPool {
-  static constexpr int value = (PM * N <= 16) ? (CMP ? 24 : 32) : (CMP ? 48 : 64);
+  static constexpr int value = (PM * N <= 16) ? (CMP ? 24 : 32) : CMP ? 48 : (PM * N <= 18) ? 32 : 64;
 };
 
 // Run totals: each lane sums its finished instances in registers; the wave
@@ -135,7 +135,15 @@ __global__ __launch_bounds__(64, CMP ? 3 : 1) void paxos_ev_kernel(EvKParams kp)
       }
       const uint32_t take = min((uint32_t)__popcll(freeb), end - next);
       const uint32_t rank = (uint32_t)__popcll(freeb & below);
-      if (((freeb >> lane) & 1ull) && rank < take) L.init(kp.p, next + rank);
+      if (((freeb >> lane) & 1ull) && rank < take) {
+        L.init(kp.p, next + rank);
+        if (__builtin_expect(L.bailed, 0)) {   // (a fuzzed P above this shape's: the general kernel's)
+          const uint32_t pos = atomicAdd(kp.bail_n, 1u);
+          if (pos < kp.bail_cap) kp.bail_ids[pos] = L.gid;
+          L.mode = M_IDLE;
+          L.bailed = false;
+        }
+      }
       next += take;
       freeb = __builtin_amdgcn_ballot_w64(L.mode == M_IDLE);
     }

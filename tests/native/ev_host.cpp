@@ -41,6 +41,10 @@ int run_shape(const pxb_config* cfg, pxb_result* out, uint32_t* dig, pxb_accepto
     L.init(p, g);
     EvOut o;
     uint64_t guard = 0;
+    if (L.bailed) {                                        // fuzzed P above the shape's (split routing)
+      bail_ids[nb++] = g;
+      continue;
+    }
     for (;;) {
       const bool done = L.step(p, o);
       ++ms;
@@ -98,9 +102,9 @@ int run_n(const pxb_config* c, pxb_result* o, uint32_t* d, pxb_acceptor_rec* a, 
 }
 
 template <int W, bool CMP>
-int run_w(const pxb_config* c, pxb_result* o, uint32_t* d, pxb_acceptor_rec* a, int64_t* t, uint32_t* b, uint32_t* nb,
-          uint64_t* ms) {
-  switch (c->n_proposers) {
+int run_w(const pxb_config* c, uint32_t pm, pxb_result* o, uint32_t* d, pxb_acceptor_rec* a, int64_t* t, uint32_t* b,
+          uint32_t* nb, uint64_t* ms) {
+  switch (pm) {
     case 1: return run_n<1, W, CMP>(c, o, d, a, t, b, nb, ms);
     case 2: return run_n<2, W, CMP>(c, o, d, a, t, b, nb, ms);
     case 3: return run_n<3, W, CMP>(c, o, d, a, t, b, nb, ms);
@@ -115,12 +119,21 @@ extern "C" int ev_host_run(const pxb_config* cfg, pxb_result* out, uint32_t* dig
   if (!cfg || !eligible(cfg)) return -1;
   const char* lv = getenv("EV_LAYOUT");                 // tests: force a layout
   const int layout = lv ? atoi(lv) : layout_for(cfg);
-  if (layout == 2 && cfg->delay_max > 7) return -1;
-  if (layout == 0 && cfg->delay_max > 7) return -1;
+  if (layout == 2 && cfg->delay_max > 8) return -1;
+  if (layout == 0 && cfg->delay_max > 8) return -1;
+  // tests: the shape's proposer capacity; below n_proposers (fuzzed batches
+  // only) it is the split routing of pxb_run_device, whose instances with more
+  // proposers than the shape bail at init
+  const char* pv = getenv("EV_PM");
+  uint32_t pm = cfg->n_proposers;
+  if (pv && atoi(pv) > 0) {
+    pm = (uint32_t)atoi(pv);
+    if (pm > cfg->n_proposers || (pm < cfg->n_proposers && !(cfg->flags & PXB_CFG_RANDOMIZE))) return -1;
+  }
   switch (layout) {
-    case 0: return run_w<8, false>(cfg, out, dig, acc, totals, bail_ids, n_bail, micro_steps);
-    case 1: return run_w<16, false>(cfg, out, dig, acc, totals, bail_ids, n_bail, micro_steps);
-    case 2: return run_w<8, true>(cfg, out, dig, acc, totals, bail_ids, n_bail, micro_steps);
+    case 0: return run_w<8, false>(cfg, pm, out, dig, acc, totals, bail_ids, n_bail, micro_steps);
+    case 1: return run_w<16, false>(cfg, pm, out, dig, acc, totals, bail_ids, n_bail, micro_steps);
+    case 2: return run_w<8, true>(cfg, pm, out, dig, acc, totals, bail_ids, n_bail, micro_steps);
   }
   return -1;
 }

@@ -14,6 +14,7 @@ import numpy as np
 import pytest
 
 import oracle_c
+import paxos_ref
 import pxb
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -147,3 +148,28 @@ def test_bailed_instances_are_reported():
     cfg = pxb.Config(seed=7, n_proposers=3, n_acceptors=9, delay_max=15, skew_max=0, step_cap=300)
     _, _, bails = check(cfg, 0, 400, max_bail_frac=1.0)
     assert len(bails) > 0
+
+
+@pytest.mark.parametrize("P,N", [(1, 9), (2, 5), (2, 9), (3, 9)])
+def test_delay8_on_8step_wheel(P, N):
+    """delay_max 8 runs on the 8-step timing wheel (due steps of the sends of
+    step s, carried-over copies included, stay within s .. s + 8)."""
+    cfg = pxb.Config(seed=0x8D + 16 * P + N, n_proposers=P, n_acceptors=N, loss_ppm=200000,
+                     delay_max=8, skew_max=3, crash_ppm=200000, crash_len_max=16,
+                     crash_start_max=16, step_cap=512)
+    check(cfg, 4321, 1200, max_bail_frac=0.05)
+
+
+@pytest.mark.parametrize("first", [0, (1 << 32) - 700])
+def test_split_shape_config5(first, monkeypatch):
+    """Config 5 split routing: a two-proposer shape runs the fuzzed instances
+    that drew P <= 2 and hands every P = 3 instance (about a third) to the
+    general kernel at init; what it runs matches the oracle exactly."""
+    monkeypatch.setenv("EV_PM", "2")
+    _, cnt, bails = check(pxb.CONFIGS[5], first, 1500, max_bail_frac=0.45)
+    assert len(bails) > 300
+    # exactly the P = 3 instances bail at init; capacity bails come on top
+    drawn = np.array([paxos_ref.instance_params(pxb.CONFIGS[5], first + g).P for g in range(1500)])
+    p3 = np.nonzero(drawn == 3)[0]
+    assert set(p3.tolist()) <= set(bails.tolist())
+    assert len(bails) - len(p3) <= 0.02 * 1500

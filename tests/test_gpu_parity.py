@@ -224,6 +224,34 @@ def test_per_lane_matches_general_kernel(gpu_lib):
     assert a[3] == b[3]
 
 
+def test_config5_split_matches_general_kernel(gpu_lib):
+    """Config 5 (fuzzed P up to 3, N = 9) runs split: the two-proposer per-lane
+    shape takes the instances that drew P <= 2 and lists the P = 3 ones for the
+    general kernel.  Identical to the general kernel alone (PXB_NO_SPLIT=1 ->
+    per-lane layout too large -> general kernel for every instance)."""
+    cfg = pxb.CONFIGS[5]
+    a = pxb.run(cfg, 4242, 60000, want_acceptors=True)
+    os.environ["PXB_NO_SPLIT"] = "1"
+    try:
+        b = pxb.run(cfg, 4242, 60000, want_acceptors=True)
+    finally:
+        del os.environ["PXB_NO_SPLIT"]
+    for x, y in zip(a[:3], b[:3]):
+        assert np.array_equal(x, y)
+    assert a[3] == b[3]
+
+
+@pytest.mark.parametrize("cap", [0, 5000])
+def test_config5_split_list_overflow(gpu_lib, cap):
+    """The split routing's id list (P = 3 instances + bails) overflowing: the
+    general kernel re-runs the chunk; exact either way."""
+    os.environ["PXB_EV_BAIL_CAP"] = str(cap)
+    try:
+        _cmp(pxb.CONFIGS[5], (1 << 32) - 7000, 14000)
+    finally:
+        del os.environ["PXB_EV_BAIL_CAP"]
+
+
 def test_device_entry_accumulates_totals(gpu_lib):
     import torch
     cfg = pxb.CONFIGS[3]
