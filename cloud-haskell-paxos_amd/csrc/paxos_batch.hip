@@ -74,23 +74,26 @@ __global__ void proposer_hook_kernel(pxb_proposer_rec* st, uint32_t n_acc, const
   nb[i] = no;
 }
 
-constexpr uint32_t QWORDS = 4;          // per-slot queue / counter words (finalize_kernel resets them)
+constexpr uint32_t QWORDS = 8;          // per-slot queue / counter words (finalize_kernel resets them)
+// queue words: [0] the general kernel's work queue, [1] the per-lane kernel's,
+// [2] its bailed-instance count; split routing: [3] the second per-lane
+// kernel's queue, [4] its bailed-instance count
+constexpr uint32_t Q_GEN = 0, Q_EV = 1, Q_BAIL = 2, Q_EV2 = 3, Q_BAIL2 = 4;
 
 // Sums the TCOPIES partial rows of the general kernel, and those of the
-// per-lane kernel unless its bailed-id list overflowed (then the general kernel
-// re-ran every instance of the chunk), into the caller's totals; zeroes them
-// and resets the queue words, so the launch slot is clean for its next use.
-// One block of TCOPIES threads; thread t reads column t % 16 of rows t/16,
-// t/16+16, ...  Queue words: [0] the general kernel's work queue, [1] the
-// per-lane kernel's, [2] its bailed-instance count.
+// per-lane kernels unless the bailed-id list the general kernel ran
+// (queue[bail_word]) overflowed (then it re-ran every instance of the chunk),
+// into the caller's totals; zeroes them and resets the queue words, so the
+// launch slot is clean for its next use.  One block of TCOPIES threads;
+// thread t reads column t % 16 of rows t/16, t/16+16, ...
 __global__ __launch_bounds__(TCOPIES) void finalize_kernel(unsigned long long* part, unsigned long long* part_ev,
-                                                            uint32_t* queue, uint32_t bail_cap,
+                                                            uint32_t* queue, uint32_t bail_word, uint32_t bail_cap,
                                                             unsigned long long* totals) {
   __shared__ unsigned long long acc[16];
   const uint32_t t = threadIdx.x;
   if (t < 16) acc[t] = 0ull;
   __syncthreads();
-  const bool ev_ok = queue[2] <= bail_cap;
+  const bool ev_ok = queue[bail_word] <= bail_cap;
   unsigned long long v = 0ull;
 #pragma unroll
   for (uint32_t j = 0; j < 16; ++j) {
@@ -204,14 +207,14 @@ static uint32_t g_qseq[64];
 // Big chunks matter: each one ends with a tail (the slowest instances of the
 // last waves, then of the bailed ones on the general kernel).
 constexpr uint64_t EV_CHUNK = 1ull << 24;
-constexpr int EV_MIN_BLOCKS = 6;
 constexpr uint32_t EV_BAIL_CAP = 1u << 20;
 // split routing (fuzzed P = 3 batches, config 5): the per-lane kernel of a
 // two-proposer shape takes the instances that drew P <= 2 and lists the P = 3
-// ones (a third) with its bails, so their list holds half a chunk
-constexpr uint32_t EV_SPLIT_BAIL_CAP = (uint32_t)(EV_CHUNK / 2);
+// ones (a third) with its bails for the three-proposer shape, so that list
+// holds half a chunk
+constexpr uint32_t EV_SPLIT_CAP = (uint32_t)(EV_CHUNK / 2);
 static uint32_t* g_bail[64][QSLOTS];
-static uint32_t g_bail_cap[64][QSLOTS];
+static uint32_t* g_split[64][QSLOTS];
 static int g_eocc[3][4][10][64];
 
 static int hip_fail(hipError_t e) {
@@ -317,15 +320,15 @@ int pxb_shutdown(void) {
     std::lock_guard<std::mutex> lk(g_mu);
     for (int d = 0; d < 64; ++d) {
       bool any = g_slots[d] != nullptr;
-      for (int k = 0; k < QSLOTS; ++k) any = any || g_bail[d][k] != nullptr;
+      for (int k = 0; k < QSLOTS; ++k) any = any || g_bail[d][k] != nullptr || g_split[d][k] != nullptr;
       if (!any) continue;
       if (hipSetDevice(d) != hipSuccess || hipDeviceSynchronize() != hipSuccess) rc = PXB_E_HIP;
       if (g_slots[d]) (void)hipFree(g_slots[d]);
       g_slots[d] = nullptr;
       for (int k = 0; k < QSLOTS; ++k) {
         if (g_bail[d][k]) (void)hipFree(g_bail[d][k]);
-        g_bail[d][k] = nullptr;
-        g_bail_cap[d][k] = 0;
+        if (g_split[d][k]) (void)hipFree(g_split[d][k]);
+        g_bail[d][k] = g_split[d][k] = nullptr;
       }
       g_qseq[d] = 0;
     }
@@ -365,31 +368,34 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
   const bool ff = !(cfg->flags & PXB_CFG_RANDOMIZE) && cfg->loss_ppm == 0 && cfg->delay_max == 1 &&
                   cfg->crash_ppm == 0;
   // faulty single-decree batches run on the per-lane kernel (paxos_ev.h), its
-  // bailed instances on the general faulty kernel, unless the per-lane layout
-  // of the topology leaves fewer than EV_MIN_BLOCKS resident waves per CU (it
-  // is latency-bound: measured 8.8 / 17.5 / 23.9 M instances/s on config 4 at
-  // 2 / 4 / 6 waves, and the P = 3, N = 9, 16-step layout fits only 3).
-  // PXB_NO_EV=1 forces the general kernel, PXB_FORCE_EV=1 the per-lane one.
+  // bailed instances on the general faulty kernel.  Per-lane beats the general
+  // kernel on every topology, even where its layout fits 3 waves per CU
+  // (MI355X, 2^22 instances, ms: config 5 148 vs 247; P = 3, N = 9 with delays
+  // to 12: 347 vs 689; P = 2, N = 9, delays to 12: 97 vs 247).
+  // PXB_NO_EV=1 forces the general kernel.
   const char* no_ev = getenv("PXB_NO_EV");
-  const char* force_ev = getenv("PXB_FORCE_EV");
   bool use_ev = !ff && !logm && ev::eligible(cfg) && !(no_ev && atoi(no_ev) > 0);
   // tests: a smaller bailed-id list, to exercise its overflow path
   const char* cap_s = getenv("PXB_EV_BAIL_CAP");
+  const uint32_t bail_cap = (cap_s && atoi(cap_s) >= 0) ? std::min<uint32_t>((uint32_t)atoi(cap_s), EV_BAIL_CAP)
+                                                      : EV_BAIL_CAP;
   kernel_fn fn = pick(cfg->n_proposers, cfg->n_acceptors, logm, ff);
   if (!fn) return PXB_E_INVAL;
   const int layout = ev::layout_for(cfg);
-  ev_kernel_ptr efn = use_ev ? ev_pick(cfg->n_proposers, cfg->n_acceptors, layout) : nullptr;
+  const ev_kernel_ptr efn = use_ev ? ev_pick(cfg->n_proposers, cfg->n_acceptors, layout) : nullptr;
   if (use_ev && !efn) return PXB_E_INVAL;
-  // fuzzed three-proposer batches whose per-lane layout fits too few waves:
-  // the two-proposer shape runs the instances that drew P <= 2, the general
-  // kernel the rest (PXB_NO_SPLIT=1 turns this off)
+  // Split routing of fuzzed three-proposer batches (config 5): the
+  // two-proposer shape's layout fits more waves (config 5: 6 vs 4 per CU), so
+  // it runs first, over the chunk, and lists the instances that drew P = 3
+  // (bailed at init) for the three-proposer shape, whose own bails go to the
+  // general kernel.  PXB_NO_SPLIT=1 turns it off.
   const char* no_split = getenv("PXB_NO_SPLIT");
   const bool may_split = use_ev && (cfg->flags & PXB_CFG_RANDOMIZE) && cfg->n_proposers == 3 &&
                          !(no_split && atoi(no_split) > 0);
+  const ev_kernel_ptr sfn = may_split ? ev_pick(2, cfg->n_acceptors, layout) : nullptr;
   bool split = false;
-  uint32_t bail_cap = EV_BAIL_CAP;
   const hipStream_t st = (hipStream_t)stream;
-  int occ, cus, eocc = 0;
+  int occ, cus, eocc = 0, socc = 0;
   {
     std::lock_guard<std::mutex> lk(g_mu);
     if (!g_cus[dev]) {
@@ -409,38 +415,29 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
     const int target = 4 * fn.occ;
     occ = std::min(o, std::max(1, target / fn.wpb));   // blocks per CU
     cus = g_cus[dev];
-    if (use_ev) {
-      int& eo = g_eocc[layout][cfg->n_proposers][cfg->n_acceptors][dev];
+    auto ev_occ = [&](ev_kernel_ptr k, uint32_t pm, int* out) -> int {
+      int& eo = g_eocc[layout][pm][cfg->n_acceptors][dev];
       if (!eo) {
         int nb = 0;
-        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)efn, 64, 0));
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k, 64, 0));
         eo = std::max(1, nb);
       }
-      eocc = eo;
-      const bool forced = force_ev && atoi(force_ev) > 0;
-      if (eocc < EV_MIN_BLOCKS && may_split && !forced) {
-        int& so = g_eocc[layout][2][cfg->n_acceptors][dev];
-        const ev_kernel_ptr sfn = ev_pick(2, cfg->n_acceptors, layout);
-        if (sfn && !so) {
-          int nb = 0;
-          HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)sfn, 64, 0));
-          so = std::max(1, nb);
-        }
-        if (sfn && so >= EV_MIN_BLOCKS) {
-          split = true;
-          efn = sfn;
-          eocc = so;
-          bail_cap = EV_SPLIT_BAIL_CAP;
-        }
+      *out = eo;
+      return PXB_OK;
+    };
+    if (use_ev) {
+      if (int rc2 = ev_occ(efn, cfg->n_proposers, &eocc)) return rc2;
+      if (sfn) {
+        if (int rc2 = ev_occ(sfn, 2, &socc)) return rc2;
+        split = socc > eocc;
       }
-      if (eocc < EV_MIN_BLOCKS && !forced) use_ev = false;
     }
-    if (cap_s && atoi(cap_s) >= 0) bail_cap = std::min<uint32_t>((uint32_t)atoi(cap_s), bail_cap);
     if (int rc2 = ensure_slots(dev)) return rc2;
     const char* cap_env = getenv("PXB_BLOCKS_PER_CU");   // tests / experiments: cap residency
     if (cap_env && atoi(cap_env) > 0) {
       occ = std::min(occ, atoi(cap_env));
       if (eocc) eocc = std::min(eocc, atoi(cap_env));
+      if (socc) socc = std::min(socc, atoi(cap_env));
     }
   }
   KParams kp;
@@ -494,7 +491,7 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
     kp.out = d_out ? reinterpret_cast<uint4*>(d_out + done) : nullptr;
     kp.dig = d_log_digest ? d_log_digest + done * cfg->n_acceptors : nullptr;
     kp.acc = d_acc ? reinterpret_cast<uint4*>(d_acc + done * cfg->n_acceptors) : nullptr;
-    uint32_t* bail = nullptr;
+    uint32_t *bail = nullptr, *slist = nullptr;
     unsigned long long* slot = nullptr;
     {
       std::lock_guard<std::mutex> lk(g_mu);
@@ -503,19 +500,12 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
       kp.part = slot;
       kp.queue = reinterpret_cast<uint32_t*>(slot + 2 * ROWS_U64);
       if (use_ev) {
-        const uint32_t need = split ? EV_SPLIT_BAIL_CAP : EV_BAIL_CAP;
-        if (g_bail_cap[dev][sidx] < need) {
-          // (the slot's previous launches on any stream may still read the old list)
-          if (g_bail[dev][sidx]) {
-            HIPCHK(hipDeviceSynchronize());
-            HIPCHK(hipFree(g_bail[dev][sidx]));
-            g_bail[dev][sidx] = nullptr;
-            g_bail_cap[dev][sidx] = 0;
-          }
-          HIPCHK(hipMalloc(&g_bail[dev][sidx], (size_t)need * sizeof(uint32_t)));
-          g_bail_cap[dev][sidx] = need;
-        }
+        if (!g_bail[dev][sidx]) HIPCHK(hipMalloc(&g_bail[dev][sidx], (size_t)EV_BAIL_CAP * sizeof(uint32_t)));
         bail = g_bail[dev][sidx];
+      }
+      if (split) {
+        if (!g_split[dev][sidx]) HIPCHK(hipMalloc(&g_split[dev][sidx], (size_t)EV_SPLIT_CAP * sizeof(uint32_t)));
+        slist = g_split[dev][sidx];
       }
     }
     // a launch that fails after an earlier one of this chunk has queued leaves
@@ -524,8 +514,11 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
       (void)hipMemsetAsync(slot, 0, SLOT_U64 * sizeof(unsigned long long), st);
       return hip_fail(e);
     };
+    uint32_t bail_word = Q_BAIL;
     if (use_ev) {
-      // the per-lane kernel over the chunk, then the general kernel over its bailed ids
+      // the per-lane kernel over the chunk, then the general kernel over its
+      // bailed ids; split: the two-proposer shape over the chunk, the
+      // three-proposer shape over its list, the general kernel over that one's
       ev::EvKParams ek;
       memset(&ek, 0, sizeof(ek));
       ek.p = ev::make_params(cfg);
@@ -535,16 +528,30 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
       ek.dig = kp.dig;
       ek.acc = kp.acc;
       ek.part = kp.part + ROWS_U64;
-      ek.queue = kp.queue + 1;
+      ek.queue = kp.queue + Q_EV;
       ek.bail_ids = bail;
-      ek.bail_n = kp.queue + 2;
+      ek.bail_n = kp.queue + Q_BAIL;
       ek.bail_cap = bail_cap;
+      if (split) {
+        ev::EvKParams sk = ek;
+        sk.bail_ids = slist;
+        sk.bail_cap = std::min<uint32_t>(bail_cap == EV_BAIL_CAP ? EV_SPLIT_CAP : bail_cap, EV_SPLIT_CAP);
+        const unsigned sgrid = (unsigned)std::min<uint64_t>((nc + 63) / 64, (uint64_t)socc * (uint64_t)cus);
+        hipLaunchKernelGGL(sfn, dim3(sgrid), dim3(64), 0, st, sk);
+        HIPCHK(hipGetLastError());
+        ek.ids = slist;
+        ek.n_ids = kp.queue + Q_BAIL;
+        ek.ids_cap = sk.bail_cap;
+        ek.queue = kp.queue + Q_EV2;
+        ek.bail_n = kp.queue + Q_BAIL2;
+        bail_word = Q_BAIL2;
+      }
       const uint64_t eres = (uint64_t)eocc * (uint64_t)cus;
       const unsigned egrid = (unsigned)std::min<uint64_t>((nc + 63) / 64, eres);
       hipLaunchKernelGGL(efn, dim3(egrid), dim3(64), 0, st, ek);
-      HIPCHK(hipGetLastError());
+      if (hipError_t e = hipGetLastError()) return fail(e);
       kp.ids = bail;
-      kp.n_ids = kp.queue + 2;
+      kp.n_ids = kp.queue + bail_word;
       kp.ids_cap = bail_cap;
       hipLaunchKernelGGL(fn.fn, dim3((unsigned)resident), dim3(64 * fn.wpb), 0, st, kp);
       if (hipError_t e = hipGetLastError()) return fail(e);
@@ -562,7 +569,7 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
       HIPCHK(hipGetLastError());
     }
     hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(TCOPIES), 0, st, kp.part, kp.part + ROWS_U64, kp.queue,
-                       bail_cap, totals);
+                       bail_word, bail_cap, totals);
     if (hipError_t e = hipGetLastError()) return fail(e);
   }
   return PXB_OK;

@@ -45,6 +45,13 @@ struct EvKParams {
   uint32_t* bail_ids;                         // ids of bailed instances (capacity bail_cap)
   uint32_t* bail_n;                           // their count, 0 on entry (may exceed bail_cap: overflow)
   uint32_t bail_cap;
+  // optional: run only the instances listed in ids[0 .. *n_ids) (another
+  // per-lane kernel's bails); a count above ids_cap (that list overflowed)
+  // runs none and marks this kernel's own list overflowed, so the general
+  // kernel re-runs the whole chunk
+  const uint32_t* ids;
+  const uint32_t* n_ids;
+  uint32_t ids_cap;
 };
 
 // response-pool words per lane of a shape (the compact layout is picked for
@@ -111,7 +118,12 @@ __global__ __launch_bounds__(64, CMP ? 3 : 1) void paxos_ev_kernel(EvKParams kp)
   L.set_keys(kp.p);
   L.mode = M_IDLE;
   L.bailed = false;
-  const uint32_t n = kp.n_instances;
+  uint32_t n = kp.n_instances;
+  if (kp.n_ids) {
+    const uint32_t c = (uint32_t)__builtin_amdgcn_readfirstlane((int)*kp.n_ids);
+    n = (c <= kp.ids_cap) ? c : 0u;
+    if (c > kp.ids_cap && blockIdx.x == 0 && lane == 0) atomicAdd(kp.bail_n, kp.bail_cap + 1u);
+  }
   const uint64_t below = (1ull << lane) - 1ull;
   uint32_t next = 0, end = 0;
   bool drained = false;
@@ -136,7 +148,7 @@ __global__ __launch_bounds__(64, CMP ? 3 : 1) void paxos_ev_kernel(EvKParams kp)
       const uint32_t take = min((uint32_t)__popcll(freeb), end - next);
       const uint32_t rank = (uint32_t)__popcll(freeb & below);
       if (((freeb >> lane) & 1ull) && rank < take) {
-        L.init(kp.p, next + rank);
+        L.init(kp.p, kp.n_ids ? kp.ids[next + rank] : next + rank);
         if (__builtin_expect(L.bailed, 0)) {   // (a fuzzed P above this shape's: the general kernel's)
           const uint32_t pos = atomicAdd(kp.bail_n, 1u);
           if (pos < kp.bail_cap) kp.bail_ids[pos] = L.gid;

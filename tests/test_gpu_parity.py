@@ -224,27 +224,31 @@ def test_per_lane_matches_general_kernel(gpu_lib):
     assert a[3] == b[3]
 
 
-def test_config5_split_matches_general_kernel(gpu_lib):
+@pytest.mark.parametrize("first", [4242, (1 << 32) - 30000])
+def test_config5_split_matches_other_routings(gpu_lib, first):
     """Config 5 (fuzzed P up to 3, N = 9) runs split: the two-proposer per-lane
-    shape takes the instances that drew P <= 2 and lists the P = 3 ones for the
-    general kernel.  Identical to the general kernel alone (PXB_NO_SPLIT=1 ->
-    per-lane layout too large -> general kernel for every instance)."""
+    shape over the chunk, the three-proposer shape over the instances that drew
+    P = 3, the general kernel over the rest's bails.  Identical to the
+    three-proposer shape alone (PXB_NO_SPLIT=1) and to the general kernel
+    alone (PXB_NO_EV=1)."""
     cfg = pxb.CONFIGS[5]
-    a = pxb.run(cfg, 4242, 60000, want_acceptors=True)
-    os.environ["PXB_NO_SPLIT"] = "1"
-    try:
-        b = pxb.run(cfg, 4242, 60000, want_acceptors=True)
-    finally:
-        del os.environ["PXB_NO_SPLIT"]
-    for x, y in zip(a[:3], b[:3]):
-        assert np.array_equal(x, y)
-    assert a[3] == b[3]
+    a = pxb.run(cfg, first, 60000, want_acceptors=True)
+    for env in ("PXB_NO_SPLIT", "PXB_NO_EV"):
+        os.environ[env] = "1"
+        try:
+            b = pxb.run(cfg, first, 60000, want_acceptors=True)
+        finally:
+            del os.environ[env]
+        for x, y in zip(a[:3], b[:3]):
+            assert np.array_equal(x, y), env
+        assert a[3] == b[3], env
 
 
 @pytest.mark.parametrize("cap", [0, 5000])
 def test_config5_split_list_overflow(gpu_lib, cap):
-    """The split routing's id list (P = 3 instances + bails) overflowing: the
-    general kernel re-runs the chunk; exact either way."""
+    """The split routing's id lists overflowing (cap 0: the P = 3 list, so the
+    second per-lane kernel runs nothing and marks its own list overflowed;
+    5000: either): the general kernel re-runs the chunk; exact either way."""
     os.environ["PXB_EV_BAIL_CAP"] = str(cap)
     try:
         _cmp(pxb.CONFIGS[5], (1 << 32) - 7000, 14000)
