@@ -15,6 +15,7 @@
 
 #include "../../include/paxos_batch.h"
 #include "paxos_ev_kernel.h"
+#include "paxos_ff1.h"
 #include "paxos_kernel.h"
 
 namespace pxb {
@@ -36,6 +37,9 @@ PXB_FOR_MODES(PXB_EXTERN, 3)
 PXB_EV_FOR(PXB_EV_EXTERN, 1, 8, false) PXB_EV_FOR(PXB_EV_EXTERN, 1, 16, false) PXB_EV_FOR(PXB_EV_EXTERN, 1, 8, true)
 PXB_EV_FOR(PXB_EV_EXTERN, 2, 8, false) PXB_EV_FOR(PXB_EV_EXTERN, 2, 16, false) PXB_EV_FOR(PXB_EV_EXTERN, 2, 8, true)
 PXB_EV_FOR(PXB_EV_EXTERN, 3, 8, false) PXB_EV_FOR(PXB_EV_EXTERN, 3, 16, false) PXB_EV_FOR(PXB_EV_EXTERN, 3, 8, true)
+#define PXB_FF1_EXTERN(N) extern template __global__ void ff1::paxos_ff1_kernel<N>(ff1::Ff1Params);
+PXB_FF1_EXTERN(2) PXB_FF1_EXTERN(3) PXB_FF1_EXTERN(4) PXB_FF1_EXTERN(5)
+PXB_FF1_EXTERN(6) PXB_FF1_EXTERN(7) PXB_FF1_EXTERN(8) PXB_FF1_EXTERN(9)
 
 // ---- single-handler hook kernels ------------------------------------------
 __global__ void acceptor_hook_kernel(pxb_acceptor_rec* st, const pxb_msg* in, pxb_msg* out, uint32_t count) {
@@ -122,6 +126,21 @@ static ev_kernel_ptr ev_pick_n(uint32_t n) {
     case 7: return ev::paxos_ev_kernel<PM, 7, W, C>;
     case 8: return ev::paxos_ev_kernel<PM, 8, W, C>;
     case 9: return ev::paxos_ev_kernel<PM, 9, W, C>;
+  }
+  return nullptr;
+}
+
+typedef void (*ff1_kernel_ptr)(ff1::Ff1Params);
+static ff1_kernel_ptr ff1_pick(uint32_t n) {
+  switch (n) {
+    case 2: return ff1::paxos_ff1_kernel<2>;
+    case 3: return ff1::paxos_ff1_kernel<3>;
+    case 4: return ff1::paxos_ff1_kernel<4>;
+    case 5: return ff1::paxos_ff1_kernel<5>;
+    case 6: return ff1::paxos_ff1_kernel<6>;
+    case 7: return ff1::paxos_ff1_kernel<7>;
+    case 8: return ff1::paxos_ff1_kernel<8>;
+    case 9: return ff1::paxos_ff1_kernel<9>;
   }
   return nullptr;
 }
@@ -216,6 +235,7 @@ constexpr uint32_t EV_SPLIT_CAP = (uint32_t)(EV_CHUNK / 2);
 static uint32_t* g_bail[64][QSLOTS];
 static uint32_t* g_split[64][QSLOTS];
 static int g_eocc[3][4][10][64];
+static int g_ff1occ[10][64];
 
 static int hip_fail(hipError_t e) {
   g_last_hip = (int)e;
@@ -379,8 +399,15 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
   const char* cap_s = getenv("PXB_EV_BAIL_CAP");
   const uint32_t bail_cap = (cap_s && atoi(cap_s) >= 0) ? std::min<uint32_t>((uint32_t)atoi(cap_s), EV_BAIL_CAP)
                                                       : EV_BAIL_CAP;
-  kernel_fn fn = pick(cfg->n_proposers, cfg->n_acceptors, logm, ff);
+  // fault-free single-proposer batches (configs 1, 2) run one instance per
+  // lane on paxos_ff1_kernel, its (never expected) bails on the general
+  // faulty kernel; PXB_NO_FF1=1 keeps them on the general fault-free kernel
+  const char* no_ff1 = getenv("PXB_NO_FF1");
+  const bool use_ff1 = ff && !logm && cfg->n_proposers == 1 && !(no_ff1 && atoi(no_ff1) > 0);
+  kernel_fn fn = pick(cfg->n_proposers, cfg->n_acceptors, logm, ff && !use_ff1);
   if (!fn) return PXB_E_INVAL;
+  const ff1_kernel_ptr ffn = use_ff1 ? ff1_pick(cfg->n_acceptors) : nullptr;
+  if (use_ff1 && !ffn) return PXB_E_INVAL;
   const int layout = ev::layout_for(cfg);
   const ev_kernel_ptr efn = use_ev ? ev_pick(cfg->n_proposers, cfg->n_acceptors, layout) : nullptr;
   if (use_ev && !efn) return PXB_E_INVAL;
@@ -403,7 +430,7 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
       HIPCHK(hipGetDeviceProperties(&prop, dev));
       g_cus[dev] = prop.multiProcessorCount;
     }
-    int& o = g_occ[(logm ? 2 : 0) + (ff ? 1 : 0)][cfg->n_proposers][cfg->n_acceptors][dev];
+    int& o = g_occ[(logm ? 2 : 0) + ((ff && !use_ff1) ? 1 : 0)][cfg->n_proposers][cfg->n_acceptors][dev];
     if (!o) {
       int nb = 0;
       HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)fn.fn, 64 * fn.wpb, 0));
@@ -425,6 +452,15 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
       *out = eo;
       return PXB_OK;
     };
+    if (use_ff1) {
+      int& fo = g_ff1occ[cfg->n_acceptors][dev];
+      if (!fo) {
+        int nb = 0;
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)ffn, 256, 0));
+        fo = std::max(1, nb);
+      }
+      eocc = fo;
+    }
     if (use_ev) {
       if (int rc2 = ev_occ(efn, cfg->n_proposers, &eocc)) return rc2;
       if (sfn) {
@@ -480,7 +516,10 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
   const uint64_t wpb = (uint64_t)fn.wpb;
   // fault-free log mode: 16-bit epochs, so every block's range (static slices:
   // every wave's) stays below 2^16 instances
-  const uint64_t chunk_max = use_ev ? std::min<uint64_t>(EV_CHUNK, (1ull << 30) - 1)
+  // (fault-free per-lane launches: all instances alike, no tail to amortise, one launch)
+  const char* fc = getenv("PXB_FF1_CHUNK");
+  const uint64_t chunk_max = use_ff1  ? ((fc && atoi(fc) > 0) ? (1ull << atoi(fc)) : (1ull << 30) - 1)
+                             : use_ev ? std::min<uint64_t>(EV_CHUNK, (1ull << 30) - 1)
                              : (ff && logm) ? std::min<uint64_t>(resident * wpb * G * 30000ull, resident * 60000ull)
                              : ff ? std::min<uint64_t>(1ull << 31, resident * wpb * G * 30000ull)
                                   : std::min<uint64_t>((1ull << 30) - 1, resident * wpb * G * 60000ull);
@@ -499,7 +538,7 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
       slot = g_slots[dev] + (size_t)sidx * SLOT_U64;
       kp.part = slot;
       kp.queue = reinterpret_cast<uint32_t*>(slot + 2 * ROWS_U64);
-      if (use_ev) {
+      if (use_ev || use_ff1) {
         if (!g_bail[dev][sidx]) HIPCHK(hipMalloc(&g_bail[dev][sidx], (size_t)EV_BAIL_CAP * sizeof(uint32_t)));
         bail = g_bail[dev][sidx];
       }
@@ -515,7 +554,35 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
       return hip_fail(e);
     };
     uint32_t bail_word = Q_BAIL;
-    if (use_ev) {
+    if (use_ff1) {
+      // the fault-free per-lane kernel over the chunk, the general kernel over its bailed ids
+      ff1::Ff1Params fp;
+      memset(&fp, 0, sizeof(fp));
+      fp.first_instance = kp.first_instance;
+      fp.k0 = kp.k0;
+      fp.k1 = kp.k1;
+      fp.skew_max = cfg->skew_max;
+      fp.step_cap = cfg->step_cap;
+      fp.n_instances = (uint32_t)nc;
+      fp.out = kp.out;
+      fp.dig = kp.dig;
+      fp.acc = kp.acc;
+      fp.part = kp.part + ROWS_U64;
+      fp.bail_ids = bail;
+      fp.bail_n = kp.queue + Q_BAIL;
+      fp.bail_cap = bail_cap;
+      const char* fb = getenv("PXB_FF1_BAIL");           // tests: hand every instance to the general kernel
+      fp.bail_all = (fb && atoi(fb) > 0) ? 1u : 0u;
+      const uint64_t fres = (uint64_t)eocc * (uint64_t)cus;
+      const unsigned fgrid = (unsigned)std::min<uint64_t>((nc + 255) / 256, fres);
+      hipLaunchKernelGGL(ffn, dim3(fgrid), dim3(256), 0, st, fp);
+      HIPCHK(hipGetLastError());
+      kp.ids = bail;
+      kp.n_ids = kp.queue + Q_BAIL;
+      kp.ids_cap = bail_cap;
+      hipLaunchKernelGGL(fn.fn, dim3((unsigned)resident), dim3(64 * fn.wpb), 0, st, kp);
+      if (hipError_t e = hipGetLastError()) return fail(e);
+    } else if (use_ev) {
       // the per-lane kernel over the chunk, then the general kernel over its
       // bailed ids; split: the two-proposer shape over the chunk, the
       // three-proposer shape over its list, the general kernel over that one's

@@ -93,7 +93,7 @@ struct Shape {
   static constexpr int BRING = POOLW + POOL;         // PM*BR halfwords: broadcast payloads
   static constexpr int WHEEL = BRING + PM * BR / 2;  // W * WW due masks
   static constexpr int WORDS = WHEEL + W * WW;
-  static_assert(W == 8 || W == 16, "wheel of 8 or 16 steps");
+  static_assert(W == 4 || W == 8 || W == 16, "wheel of 4, 8 or 16 steps");
   static_assert(NIN <= 32 && NLQ <= 32, "masks are 32-bit");
   static_assert(RD + 4 <= 32, "response-link word");
   static_assert(QL + QLB <= 31, "request-link word");

@@ -1,0 +1,359 @@
+// paxos_ff1.h — per-lane kernel for fault-free single-proposer batches
+// (BASELINE configs 1 and 2: P = 1, no loss, delay 1, no crash windows; Tick
+// skew allowed), one lane per instance.
+//
+// Fault-free means every message sent in step s is handled in step s + 1
+// (docs/SEMANTICS.md §5-§6), so an instance's in-flight state is just the
+// broadcasts its proposer made in the previous step (all N copies carry the
+// same payload) and one reply per acceptor.  A lane keeps all of it — N
+// acceptors (Server.hs:24-31), the proposer's ClientState (Client.hs:58-67),
+// the in-flight messages and the run totals — in registers and runs each step
+// as the two phases of §6:
+//   proposer phase   its Tick at the skew step (handleTick, Client.hs:196-207),
+//                    then the replies of acceptors 0..N-1 in order
+//                    (handleServerResponse, Client.hs:125-189);
+//   acceptor phase   acceptors 0..N-1 each handle the previous step's
+//                    broadcasts in order (handleClientRequest, Server.hs:51-78)
+//                    and reply (Common.hs:36-39 sendToAllServers / send).
+// The two phases of one step are independent (every send is due one step
+// later), so the proposer phase runs first and the acceptor phase overwrites
+// the replies it consumed.  The handlers are the shared ones of
+// paxos_device.h.
+//
+// Compared with the general kernel (one lane per (instance, acceptor), the
+// proposer state replicated in the instance's N lanes and its fold done with
+// cross-lane ballots and DPP reductions), nothing is replicated and nothing
+// crosses lanes.  An instance this layout cannot hold (more than two
+// broadcasts in one step, two replies from one acceptor in one step, a log of
+// 31 entries: none happens with one proposer) is "bailed" to the general
+// kernel, like the per-lane event kernel's (paxos_ev_kernel.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "paxos_ev_kernel.h"
+
+namespace pxb {
+namespace ff1 {
+
+struct Ff1Params {
+  uint64_t first_instance;
+  uint32_t k0, k1;                            // Philox key (Tick skew draws)
+  uint32_t skew_max, step_cap;
+  uint32_t n_instances;
+  uint4* out;                                 // pxb_result records (nullable)
+  uint32_t* dig;                              // log digests (nullable)
+  uint4* acc;                                 // final acceptor records (nullable)
+  unsigned long long* part;                   // ev::EV_TCOPIES partial run-total rows
+  uint32_t* bail_ids;                         // ids of bailed instances (capacity bail_cap)
+  uint32_t* bail_n;                           // their count, 0 on entry
+  uint32_t bail_cap;
+  uint32_t bail_all;                          // tests: bail every instance (exercises the general kernel)
+};
+
+// request payload bytes (SEMANTICS §8): Ask 8, Propose 12, Execute 8
+__device__ __forceinline__ uint32_t req_bytes(uint32_t kind) { return kind == PROPOSE ? 12u : 8u; }
+// response payload bytes: Round1OK 16, HaveTicket 8, Round2Success 4
+__device__ __forceinline__ uint32_t rsp_bytes(uint32_t kind) { return 16u >> kind; }
+
+// The lanes of a wave run in lockstep (every instance of a skew-free batch
+// takes the same steps), so the handlers branch on the message kind and the
+// proposer state: a wave runs only the path its instances are on (measured on
+// MI355X: 10 % faster than the predicated select form of the event kernel,
+// which pays for every path of every handler).
+constexpr uint32_t TM = 0x3FFFu;              // ticket field
+
+template <int N>
+struct Ff1Lane {
+  // acceptors, packed: t_max [13:0] | t_store [27:14] | val [29:28] | dead [30]
+  // (tickets <= step_cap <= 8192 < 2^14, SEMANTICS §6; commands travel as the
+  // clientId, 0 = Nothing); log lengths; running log digests
+  uint32_t aw[N], llen[N], accd[N];
+  // the proposer (clientId 1): its command travels as the clientId, 1
+  PropState S;
+  // in flight: the broadcasts of the previous step, the replies of the previous step
+  uint32_t nreq;                              // 0..2
+  uint32_t req[2];                            // x [13:0] | z [29:28] | kind [31:30]
+  uint32_t rmask;                             // acceptors with a reply in flight
+  uint32_t rsp[N];                            // x [13:0] | y [27:14] | z [29:28] | kind [31:30]
+  // per-instance outputs and counters
+  uint32_t skew, lflags, rounds, msgs, execs, canon, dval, dtick;
+  unsigned long long clog;                    // canonical log, 2-bit values (divergence, SEMANTICS §7)
+  uint32_t clog_len;
+  bool bailed;
+
+  __device__ __forceinline__ void init(const Ff1Params& kp, uint64_t inst) {
+    skew = 0u;
+    if (kp.skew_max > 0u) {                                     // SEMANTICS §4, purpose "skew"
+      const uint4 w = philox((uint32_t)inst, (uint32_t)(inst >> 32), 0u, 2u << 24, kp.k0, kp.k1);
+      skew = mulhi_n(w.x, kp.skew_max + 1u);
+    }
+#pragma unroll
+    for (int a = 0; a < N; ++a) {
+      aw[a] = 0u;                                               // Server.hs:46
+      llen[a] = 0u;
+      accd[a] = 0x811C9DC5u;
+    }
+    S = PropState{0, 0u, 0u, IDLE, 0, 0u, 0, 0u, 0u};           // Client.hs:90-95
+    nreq = req[0] = req[1] = 0u;
+    rmask = 0u;
+    lflags = rounds = msgs = execs = canon = dval = dtick = 0u;
+    clog = 0ull;
+    clog_len = 0u;
+    bailed = false;
+  }
+
+  // a broadcast of the proposer phase (Client.hs:122-123): N copies, due next
+  // step, as one word x [13:0] | z [29:28] | kind [31:30] (predicated on go)
+  __device__ __forceinline__ void bcast(bool go, uint32_t kind, uint32_t x, uint32_t z, uint32_t& n0, uint32_t& n1,
+                                        uint32_t& nn) {
+    const uint32_t w = x | (z << 28) | (kind << 30);
+    bailed = bailed | (go & (nn >= 2u));
+    n0 = (go & (nn == 0u)) ? w : n0;
+    n1 = (go & (nn == 1u)) ? w : n1;
+    nn += go ? 1u : 0u;
+    msgs += go ? (uint32_t)N : 0u;
+    rounds += (go & (kind == ASK)) ? 1u : 0u;
+    const bool ex = go & (kind == EXECUTE);
+    execs += ex ? 1u : 0u;
+    const bool first = ex & (dval == 0u);                    // the first Execute decides (SEMANTICS §7)
+    dval = first ? S.r2_v : dval;
+    dtick = first ? x : dtick;
+  }
+
+  // handleServerResponse (Client.hs:125-189) of acceptor a's reply, one
+  // function per reply kind, predicated on go (Q3: the sender is not checked)
+  __device__ __forceinline__ void fold_r1ok(bool go, int a, uint32_t& n0, uint32_t& n1, uint32_t& nn) {
+    const uint32_t r = rsp[a];
+    const int32_t px = (int32_t)(r & TM), py = (int32_t)((r >> 14) & TM);
+    const uint32_t pz = (r >> 28) & 3u;
+    canon += go ? 2u * 16u : 0u;
+    const bool o_go = go & (S.rs == ROUND1) & (S.ticket == px);        // :144-145
+    const uint32_t K1 = S.acks + 1u;                                     // :146
+    const bool take = (S.mr_v == 0u) | ((pz != 0u) & !(S.mr_t >= py));   // mr <> MostRecent (Common.hs:61-65)
+    const int32_t mt = take ? py : S.mr_t;
+    const uint32_t mv = take ? pz : S.mr_v;
+    const bool maj = o_go & (K1 > ((uint32_t)N >> 1));                  // :152-154, haveMajority :191-194
+    S.r2_t = maj ? px : S.r2_t;                                         // :157-167 (Q5: pending whenever mr is Just)
+    S.r2_v = maj ? ((mv == 0u) ? S.cmd : mv) : S.r2_v;
+    S.pending = maj ? ((mv != 0u) ? 1u : 0u) : S.pending;
+    S.acks = maj ? 0u : (o_go ? K1 : S.acks);                           // :168
+    S.rs = maj ? ROUND2 : S.rs;                                         // :169
+    S.mr_t = maj ? 0 : (o_go ? mt : S.mr_t);
+    S.mr_v = maj ? 0u : (o_go ? mv : S.mr_v);
+    bcast(maj, PROPOSE, (uint32_t)px, S.r2_v, n0, n1, nn);              // :170
+  }
+  __device__ __forceinline__ void fold_have(bool go, int a, uint32_t& n0, uint32_t& n1, uint32_t& nn) {
+    const int32_t px = (int32_t)(rsp[a] & TM);
+    canon += go ? 2u * 8u : 0u;
+    const bool h = go & (S.rs != IDLE) & (px >= S.ticket);               // :130-132
+    S.ticket = h ? px + 1 : S.ticket;                                    // :134-135
+    S.acks = h ? 0u : S.acks;                                            // :137
+    S.rs = h ? ROUND1 : S.rs;                                            // :138
+    S.mr_t = h ? 0 : S.mr_t;
+    S.mr_v = h ? 0u : S.mr_v;
+    bcast(h, ASK, (uint32_t)S.ticket, 0u, n0, n1, nn);                   // :140
+  }
+  __device__ __forceinline__ void fold_r2s(bool go, uint32_t& n0, uint32_t& n1, uint32_t& nn) {
+    canon += go ? 2u * 4u : 0u;
+    const bool s_go = go & (S.rs == ROUND2);                             // :172-174 (no ticket: Q2)
+    const uint32_t K1 = S.acks + 1u;                                     // :175
+    const bool maj = s_go & (K1 > ((uint32_t)N >> 1));                  // :176-177
+    const bool restart = maj & (S.pending != 0u);                        // :179
+    bcast(maj, EXECUTE, (uint32_t)S.ticket, 0u, n0, n1, nn);             // :178 Execute (s ^. ticket)
+    S.ticket = restart ? S.ticket + 1 : S.ticket;                        // :182
+    S.acks = maj ? 0u : (s_go ? K1 : S.acks);                           // :183 / :188
+    S.rs = restart ? ROUND1 : (maj ? IDLE : S.rs);                       // :184 / :189
+    S.mr_t = restart ? 0 : S.mr_t;
+    S.mr_v = restart ? 0u : S.mr_v;
+    S.cmd = (maj & !restart) ? 0u : S.cmd;                               // :187
+    bcast(restart, ASK, (uint32_t)S.ticket, 0u, n0, n1, nn);             // :185
+  }
+
+  // the reply of acceptor a, due next step (predicated on go)
+  __device__ __forceinline__ void reply(bool go, int a, uint32_t w, uint32_t& nmask) {
+    bailed = bailed | (go & (((nmask >> a) & 1u) != 0u));     // (one reply per acceptor per step)
+    nmask |= go ? (1u << a) : 0u;
+    rsp[a] = go ? w : rsp[a];
+    msgs += go ? 1u : 0u;
+  }
+
+  // handleClientRequest (Server.hs:51-78) of one broadcast by every acceptor,
+  // in acceptor order: one branch on the broadcast's kind, then selects (the
+  // acceptors of one instance may differ: a dead one, a refused ticket)
+  __device__ __forceinline__ void accept_all(uint32_t q, uint32_t& nmask) {
+    const uint32_t kind = q >> 30, z = (q >> 28) & 3u, x = q & TM;
+    const uint32_t pay = req_bytes(kind);
+    if (kind == ASK) {                                        // :54-62
+#pragma unroll
+      for (int a = 0; a < N; ++a) {
+        const uint32_t A = aw[a], t_max = A & TM;
+        const bool live = (A >> 30) == 0u;
+        canon += live ? 2u * pay + 32u : pay;
+        const bool grant = live & !(t_max >= x);              // :56
+        aw[a] = grant ? (A & ~TM) | x : A;                    // :60
+        // :61-62 Round1OK t prop (t, t_store, val), or :58 HaveTicket T_max
+        reply(live, a, grant ? (x | (A & (0xFFFFu << 14)) | (R1OK << 30)) : (t_max | (HAVE << 30)), nmask);
+      }
+    } else if (kind == PROPOSE) {                             // :64-71
+#pragma unroll
+      for (int a = 0; a < N; ++a) {
+        const uint32_t A = aw[a], t_max = A & TM;
+        const bool live = (A >> 30) == 0u;
+        canon += live ? 2u * pay + 32u : pay;
+        const bool acc = live & (x == t_max);                 // :66 (equality, not >=)
+        aw[a] = acc ? t_max | (x << 14) | (z << 28) : A;      // :68 prop := Just (t, c)
+        reply(live, a, acc ? (R2S << 30) : (t_max | (HAVE << 30)), nmask);   // :70 / :71
+      }
+    } else {                                                  // Execute, :73-78 (no reply)
+#pragma unroll
+      for (int a = 0; a < N; ++a) {
+        const uint32_t A = aw[a], v = (A >> 28) & 3u;
+        const bool live = (A >> 30) == 0u;
+        canon += live ? 2u * pay + 32u : pay;
+        const bool hit = live & ((A & TM) == x);              // :75
+        const bool panic = hit & (v == 0u);                   // :76 pattern failure: dead forever (Q6)
+        const bool run = hit & (v != 0u);                     // :77-78 executed <>= [c]; prop := Nothing
+        lflags |= panic ? (uint32_t)PXB_F_PANIC : 0u;
+        aw[a] = run ? (A & TM) : (panic ? (A | (1u << 30)) : A);
+        bailed = bailed | (run & (llen[a] >= 31u));
+        accd[a] = run ? fnv_u32(accd[a], (v << 24) | 1u) : accd[a];
+        const bool old = llen[a] < clog_len;
+        lflags |= (run & old & (((uint32_t)(clog >> (2u * llen[a])) & 3u) != v)) ? (uint32_t)PXB_F_LOG_DIVERGENCE
+                                                                                  : 0u;
+        clog |= (run & !old) ? (unsigned long long)v << (2u * llen[a]) : 0ull;
+        clog_len += (run & !old) ? 1u : 0u;
+        llen[a] += run ? 1u : 0u;
+      }
+    }
+  }
+
+  // one step (SEMANTICS §6); returns true when the instance ended after it
+  __device__ __forceinline__ bool step(uint32_t s, uint32_t step_cap, uint32_t& steps, bool& capped) {
+    // ---- proposer phase: its Tick, then the replies in acceptor order ----
+    uint32_t n0 = 0u, n1 = 0u, nn = 0u;
+    const bool tick = s == skew;
+    canon += (tick | (rmask != 0u)) ? 48u : 0u;
+    if (tick) {                                               // handleTick, Client.hs:196-207
+      const bool t_go = S.rs == IDLE;                         // :199
+      S.ticket = t_go ? S.ticket + 1 : S.ticket;              // :200
+      S.cmd = t_go ? 1u : S.cmd;                              // :202-204 "c1.1" as clientId 1
+      S.acks = t_go ? 0u : S.acks;                            // :205
+      S.rs = t_go ? ROUND1 : S.rs;                            // :206
+      S.mr_t = t_go ? 0 : S.mr_t;
+      S.mr_v = t_go ? 0u : S.mr_v;
+      bcast(t_go, ASK, (uint32_t)S.ticket, 0u, n0, n1, nn);   // :207
+    }
+    if (rmask != 0u) {
+      // the replies of one step usually share a kind (every lane of a wave in
+      // the same round): one branch, then the predicated handler of that kind
+      uint32_t kinds = 0u;
+#pragma unroll
+      for (int a = 0; a < N; ++a) kinds |= ((rmask >> a) & 1u) ? 1u << (rsp[a] >> 30) : 0u;
+      if (kinds == (1u << R1OK)) {
+#pragma unroll
+        for (int a = 0; a < N; ++a) fold_r1ok(((rmask >> a) & 1u) != 0u, a, n0, n1, nn);
+      } else if (kinds == (1u << R2S)) {
+#pragma unroll
+        for (int a = 0; a < N; ++a) fold_r2s(((rmask >> a) & 1u) != 0u, n0, n1, nn);
+      } else {
+#pragma unroll
+        for (int a = 0; a < N; ++a) {
+          const bool go = ((rmask >> a) & 1u) != 0u;
+          const uint32_t k = rsp[a] >> 30;
+          fold_r1ok(go & (k == R1OK), a, n0, n1, nn);
+          fold_have(go & (k == HAVE), a, n0, n1, nn);
+          fold_r2s(go & (k == R2S), n0, n1, nn);
+        }
+      }
+    }
+    // ---- acceptor phase: the previous step's broadcasts, in order ----
+    uint32_t nmask = 0u;
+    if (nreq > 0u) accept_all(req[0], nmask);
+    if (__builtin_expect(nreq > 1u, 0)) accept_all(req[1], nmask);
+    rmask = nmask;
+    nreq = nn;
+    req[0] = n0;
+    req[1] = n1;
+    // ---- end of step ----
+    const bool quiet = (nreq == 0u) & (rmask == 0u) & (s >= skew);
+    capped = !quiet & (s + 1u >= step_cap);
+    steps = s + 1u;
+    return quiet | capped;
+  }
+
+  __device__ __forceinline__ void finish(bool capped, uint32_t steps, uint32_t (&res)[4], uint32_t& f) {
+    f = lflags | (capped ? (uint32_t)PXB_F_STEP_CAP : 0u) | (dval ? 0u : (uint32_t)PXB_F_UNDECIDED) |
+        ((!capped && S.rs != IDLE) ? (uint32_t)PXB_F_STUCK : 0u);
+    canon += 16u + 4u * (uint32_t)N;
+    res[0] = dval ? ((dval << 24) | 1u) : 0u;
+    res[1] = dval ? dtick : 0u;
+    res[2] = rounds;
+    res[3] = (f & 0xFFu) | (steps << 16);
+  }
+
+  __device__ __forceinline__ uint4 record(int a) const {
+    const uint32_t A = aw[a], val = (A >> 28) & 3u;
+    return make_uint4(A & TM, (A >> 14) & TM, val ? ((val << 24) | 1u) : 0u, llen[a] | ((A >> 30) << 31));
+  }
+};
+
+// Grid-stride over the launch's instances, one per lane at a time; the lanes
+// of a wave run in lockstep (every instance of a skew-free batch takes the
+// same steps).  Run totals as in the per-lane event kernel: register sums,
+// wave-reduced into one of EV_TCOPIES partial rows.
+template <int N>
+__global__ __launch_bounds__(256) void paxos_ff1_kernel(Ff1Params kp) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const uint32_t n_waves = gridDim.x * (blockDim.x >> 6);
+  unsigned long long* const trow = kp.part + (size_t)(wave % ev::EV_TCOPIES) * 16u;
+  ev::EvTotals tot;
+  tot.clear();
+  for (uint32_t w0 = wave * 64u; w0 < kp.n_instances; w0 += n_waves * 64u) {
+    // (wave-uniform: flush the sums before any could wrap)
+    if (__builtin_amdgcn_ballot_w64(tot.c[0] >= ev::EV_FLUSH) != 0ull) tot.flush(trow, lane);
+    const uint32_t g = w0 + lane;
+    if (g < kp.n_instances) {
+      Ff1Lane<N> L;
+      L.init(kp, kp.first_instance + g);
+      L.bailed = kp.bail_all != 0u;
+      uint32_t steps = 0u;
+      bool capped = false;
+#pragma nounroll
+      for (uint32_t s = 0;; ++s)
+        if (L.step(s, kp.step_cap, steps, capped) || L.bailed) break;
+      if (__builtin_expect(L.bailed, 0)) {
+        const uint32_t pos = atomicAdd(kp.bail_n, 1u);
+        if (pos < kp.bail_cap) kp.bail_ids[pos] = g;
+      } else {
+        uint32_t res[4], f;
+        L.finish(capped, steps, res, f);
+        tot.c[0] += 1u;
+        tot.c[1] += (f & PXB_F_UNDECIDED) ? 1u : 0u;
+        tot.c[2] += (f & PXB_F_STUCK) ? 1u : 0u;
+        tot.c[3] += (f & PXB_F_PANIC) ? 1u : 0u;
+        tot.c[4] += (f & PXB_F_LOG_DIVERGENCE) ? 1u : 0u;
+        tot.c[5] += (f & PXB_F_STEP_CAP) ? 1u : 0u;
+        tot.c[6] += L.rounds;
+        tot.c[7] += steps;
+        tot.c[8] += L.msgs;
+        tot.c[9] += L.execs;
+        tot.canon += L.canon;
+        if (kp.out) kp.out[g] = make_uint4(res[0], res[1], res[2], res[3]);
+        if (kp.dig) {
+#pragma unroll
+          for (int a = 0; a < N; ++a) kp.dig[(uint64_t)g * N + a] = fnv_u32(L.accd[a], L.llen[a]);
+        }
+        if (kp.acc) {
+#pragma unroll
+          for (int a = 0; a < N; ++a) kp.acc[(uint64_t)g * N + a] = L.record(a);
+        }
+      }
+    }
+  }
+  tot.flush(trow, lane);
+}
+
+}  // namespace ff1
+}  // namespace pxb

@@ -317,6 +317,9 @@ __global__ __launch_bounds__((Shape<PM, N, LOGM, FF>::block), (Occ<PM, FF>::wave
   const uint32_t n_listed = (!FF && kp.n_ids) ? (uint32_t)__builtin_amdgcn_readfirstlane((int)*kp.n_ids) : 0u;
   const bool listed = !FF && kp.n_ids && n_listed <= kp.ids_cap;
   const uint32_t n = listed ? n_listed : kp.n_instances;
+  // an empty list (the usual case behind the per-lane kernels): leave at once,
+  // before any wave touches the work queue (grid-uniform)
+  if (listed && n == 0u) return;
   // faulty kernels: chunks from the device work queue (DYN); fault-free
   // kernels: one-generation chunks of the block's contiguous range from an
   // LDS counter (BQ); diagnostic builds: a static slice per wave

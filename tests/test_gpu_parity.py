@@ -256,6 +256,35 @@ def test_config5_split_list_overflow(gpu_lib, cap):
         del os.environ["PXB_EV_BAIL_CAP"]
 
 
+@pytest.mark.parametrize("c,n", [(1, 5000), (2, 20000), ("skew", 9000)])
+def test_ff1_bails_run_on_general_kernel(gpu_lib, c, n):
+    """Fault-free single-proposer batches run one instance per lane
+    (paxos_ff1.h); an instance it hands back runs on the general faulty
+    kernel.  PXB_FF1_BAIL=1 hands back every instance: still exact."""
+    cfg = pxb.Config(seed=0xFF1, n_proposers=1, n_acceptors=7, skew_max=5) if c == "skew" else pxb.CONFIGS[c]
+    os.environ["PXB_FF1_BAIL"] = "1"
+    try:
+        _cmp(cfg, 123, n)
+    finally:
+        del os.environ["PXB_FF1_BAIL"]
+
+
+@pytest.mark.parametrize("N", [2, 3, 4, 5, 6, 7, 8, 9])
+def test_ff1_matches_general_fault_free_kernel(gpu_lib, N):
+    """The fault-free per-lane kernel against the general fault-free kernel
+    (PXB_NO_FF1=1) and the oracle, with Tick skew and a step cap that cuts
+    some instances."""
+    cfg = pxb.Config(seed=0xF0 + N, n_proposers=1, n_acceptors=N, skew_max=9, step_cap=12)
+    a = _cmp(cfg, (1 << 32) - 5000, 10000)
+    os.environ["PXB_NO_FF1"] = "1"
+    try:
+        b = _cmp(cfg, (1 << 32) - 5000, 10000)
+    finally:
+        del os.environ["PXB_NO_FF1"]
+    assert np.array_equal(a[0], b[0]) and a[1] == b[1]
+    assert a[1]["step_cap"] > 0 and a[1]["decided"] > 0
+
+
 def test_device_entry_accumulates_totals(gpu_lib):
     import torch
     cfg = pxb.CONFIGS[3]

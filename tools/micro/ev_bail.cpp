@@ -51,9 +51,26 @@ void run(const char* name, const pxb_config* cfg, uint32_t only_p = 0) {
 
 int main(int argc, char** argv) {
   pxb_config c{};
-  c.seed = 0x5EED0005;
   c.first_instance = argc > 2 ? strtoull(argv[2], 0, 0) : 0;
   c.n_instances = argc > 1 ? strtoull(argv[1], 0, 0) : 20000;
+  const int which = argc > 3 ? atoi(argv[3]) : 5;
+  if (which == 4) {                       // BASELINE config 4
+    c.seed = 0x5EED0004;
+    c.n_proposers = 2;
+    c.n_acceptors = 7;
+    c.delay_max = 4;
+    c.crash_ppm = 200000;
+    c.crash_len_max = 16;
+    c.crash_start_max = 8;
+    c.step_cap = 256;
+    run<2, 7, 24, 8, true>("c4 cur <2,7,24,W8,cmp>", &c);
+    run<2, 7, 24, 4, true>("c4 <2,7,24,W4,cmp>", &c);
+    run<2, 7, 22, 4, true>("c4 <2,7,22,W4,cmp>", &c);
+    run<2, 7, 20, 4, true>("c4 <2,7,20,W4,cmp>", &c);
+    run<2, 7, 16, 4, true>("c4 <2,7,16,W4,cmp>", &c);
+    return 0;
+  }
+  c.seed = 0x5EED0005;
   c.n_proposers = 3;
   c.n_acceptors = 9;
   c.loss_ppm = 300000;
@@ -64,15 +81,9 @@ int main(int argc, char** argv) {
   c.skew_max = 3;
   c.step_cap = 512;
   c.flags = PXB_CFG_RANDOMIZE;
-  run<3, 9, 64, 16, false>("cur <3,9,64,W16,full>", &c);
   run<3, 9, 64, 8, false>("P=3 <3,9,64,W8,full>", &c, 3);
-  run<2, 9, 64, 8, false>("P=2 <2,9,64,W8,full>", &c, 2);
-  run<2, 9, 48, 8, false>("P=2 <2,9,48,W8,full>", &c, 2);
+  run<3, 9, 48, 8, false>("P=3 <3,9,48,W8,full>", &c, 3);
   run<2, 9, 32, 8, false>("P=2 <2,9,32,W8,full>", &c, 2);
   run<2, 9, 32, 8, true>("P=2 <2,9,32,W8,cmp>", &c, 2);
-  run<1, 9, 64, 8, false>("P=1 <1,9,64,W8,full>", &c, 1);
-  run<1, 9, 32, 8, false>("P=1 <1,9,32,W8,full>", &c, 1);
-  run<1, 9, 24, 8, true>("P=1 <1,9,24,W8,cmp>", &c, 1);
-  run<1, 9, 16, 8, true>("P=1 <1,9,16,W8,cmp>", &c, 1);
   return 0;
 }

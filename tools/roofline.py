@@ -22,7 +22,7 @@ from collections import defaultdict
 CUS = 256
 PEAK_CLOCK_HZ = 2.4e9
 VALU_PER_CU_CYCLE = 2.0
-KERNEL_TAGS = ("paxos_ev_kernel", "paxos_batch_kernel", "finalize_kernel")
+KERNEL_TAGS = ("paxos_ev_kernel", "paxos_ff1_kernel", "paxos_batch_kernel", "finalize_kernel")
 
 
 def _tag(name):
