@@ -123,7 +123,9 @@ struct Ff1Lane {
 
   // handleServerResponse (Client.hs:125-189) of acceptor a's reply, one
   // function per reply kind, predicated on go (Q3: the sender is not checked)
-  __device__ __forceinline__ void fold_r1ok(bool go, int a, uint32_t& n0, uint32_t& n1, uint32_t& nn) {
+  // (returns whether it reached the majority: its Propose is then the pass's
+  // only broadcast, Round2 ignores further Round1OKs)
+  __device__ __forceinline__ bool fold_r1ok(bool go, int a) {
     const uint32_t r = rsp[a];
     const int32_t px = (int32_t)(r & TM), py = (int32_t)((r >> 14) & TM);
     const uint32_t pz = (r >> 28) & 3u;
@@ -141,7 +143,7 @@ struct Ff1Lane {
     S.rs = maj ? ROUND2 : S.rs;                                         // :169
     S.mr_t = maj ? 0 : (o_go ? mt : S.mr_t);
     S.mr_v = maj ? 0u : (o_go ? mv : S.mr_v);
-    bcast(maj, PROPOSE, (uint32_t)px, S.r2_v, n0, n1, nn);              // :170
+    return maj;                                                         // :170 Propose (r2_t, r2_v)
   }
   __device__ __forceinline__ void fold_have(bool go, int a, uint32_t& n0, uint32_t& n1, uint32_t& nn) {
     const int32_t px = (int32_t)(rsp[a] & TM);
@@ -154,20 +156,28 @@ struct Ff1Lane {
     S.mr_v = h ? 0u : S.mr_v;
     bcast(h, ASK, (uint32_t)S.ticket, 0u, n0, n1, nn);                   // :140
   }
-  __device__ __forceinline__ void fold_r2s(bool go, uint32_t& n0, uint32_t& n1, uint32_t& nn) {
+  // (returns whether it reached the majority: Execute, then with a pending
+  // command the restart's AskForTicket; Idle / Round1 ignore further ones)
+  __device__ __forceinline__ bool fold_r2s(bool go, bool& restart) {
     canon += go ? 2u * 4u : 0u;
     const bool s_go = go & (S.rs == ROUND2);                             // :172-174 (no ticket: Q2)
     const uint32_t K1 = S.acks + 1u;                                     // :175
     const bool maj = s_go & (K1 > ((uint32_t)N >> 1));                  // :176-177
-    const bool restart = maj & (S.pending != 0u);                        // :179
-    bcast(maj, EXECUTE, (uint32_t)S.ticket, 0u, n0, n1, nn);             // :178 Execute (s ^. ticket)
+    restart = maj & (S.pending != 0u);                                   // :179
     S.ticket = restart ? S.ticket + 1 : S.ticket;                        // :182
     S.acks = maj ? 0u : (s_go ? K1 : S.acks);                           // :183 / :188
     S.rs = restart ? ROUND1 : (maj ? IDLE : S.rs);                       // :184 / :189
     S.mr_t = restart ? 0 : S.mr_t;
     S.mr_v = restart ? 0u : S.mr_v;
     S.cmd = (maj & !restart) ? 0u : S.cmd;                               // :187
-    bcast(restart, ASK, (uint32_t)S.ticket, 0u, n0, n1, nn);             // :185
+    return maj;
+  }
+  // the broadcasts of a Round2Success majority: Execute (s ^. ticket), :178,
+  // and after a restart AskForTicket with the new ticket, :185
+  __device__ __forceinline__ void r2s_bcast(bool maj, bool restart, uint32_t& n0, uint32_t& n1, uint32_t& nn) {
+    const uint32_t t = (uint32_t)S.ticket;
+    bcast(maj, EXECUTE, restart ? t - 1u : t, 0u, n0, n1, nn);
+    bcast(restart, ASK, t, 0u, n0, n1, nn);
   }
 
   // the reply of acceptor a, due next step (predicated on go)
@@ -251,19 +261,33 @@ struct Ff1Lane {
 #pragma unroll
       for (int a = 0; a < N; ++a) kinds |= ((rmask >> a) & 1u) ? 1u << (rsp[a] >> 30) : 0u;
       if (kinds == (1u << R1OK)) {
+        bool m = false;
 #pragma unroll
-        for (int a = 0; a < N; ++a) fold_r1ok(((rmask >> a) & 1u) != 0u, a, n0, n1, nn);
+        for (int a = 0; a < N; ++a) m = m | fold_r1ok(((rmask >> a) & 1u) != 0u, a);
+        bcast(m, PROPOSE, (uint32_t)S.r2_t, S.r2_v, n0, n1, nn);
       } else if (kinds == (1u << R2S)) {
+        bool m = false, re = false;
 #pragma unroll
-        for (int a = 0; a < N; ++a) fold_r2s(((rmask >> a) & 1u) != 0u, n0, n1, nn);
+        for (int a = 0; a < N; ++a) {
+          bool r;
+          m = m | fold_r2s(((rmask >> a) & 1u) != 0u, r);
+          re = re | r;
+        }
+        r2s_bcast(m, re, n0, n1, nn);
       } else {
 #pragma unroll
         for (int a = 0; a < N; ++a) {
           const bool go = ((rmask >> a) & 1u) != 0u;
           const uint32_t k = rsp[a] >> 30;
-          fold_r1ok(go & (k == R1OK), a, n0, n1, nn);
-          fold_have(go & (k == HAVE), a, n0, n1, nn);
-          fold_r2s(go & (k == R2S), n0, n1, nn);
+          if (go & (k == R1OK)) {
+            if (fold_r1ok(true, a)) bcast(true, PROPOSE, (uint32_t)S.r2_t, S.r2_v, n0, n1, nn);
+          } else if (go & (k == HAVE)) {
+            fold_have(true, a, n0, n1, nn);
+          } else if (go) {
+            bool r;
+            const bool m = fold_r2s(true, r);
+            r2s_bcast(m, r, n0, n1, nn);
+          }
         }
       }
     }
