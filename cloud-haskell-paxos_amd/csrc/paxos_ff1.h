@@ -25,7 +25,7 @@
 // cross-lane ballots and DPP reductions), nothing is replicated and nothing
 // crosses lanes.  An instance this layout cannot hold (more than two
 // broadcasts in one step, two replies from one acceptor in one step, a log of
-// 31 entries: none happens with one proposer) is "bailed" to the general
+// 17 entries: none happens with one proposer) is "bailed" to the general
 // kernel, like the per-lane event kernel's (paxos_ev_kernel.h).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -75,10 +75,11 @@ struct Ff1Lane {
   uint32_t nreq;                              // 0..2
   uint32_t req[2];                            // x [13:0] | z [29:28] | kind [31:30]
   uint32_t rmask;                             // acceptors with a reply in flight
+  uint32_t rkinds;                            // their kinds, bit 1 << kind
   uint32_t rsp[N];                            // x [13:0] | y [27:14] | z [29:28] | kind [31:30]
   // per-instance outputs and counters
   uint32_t skew, lflags, rounds, msgs, execs, canon, dval, dtick;
-  unsigned long long clog;                    // canonical log, 2-bit values (divergence, SEMANTICS §7)
+  uint32_t clog;                              // canonical log, 2-bit values (divergence, SEMANTICS §7)
   uint32_t clog_len;
   bool bailed;
 
@@ -96,9 +97,9 @@ struct Ff1Lane {
     }
     S = PropState{0, 0u, 0u, IDLE, 0, 0u, 0, 0u, 0u};           // Client.hs:90-95
     nreq = req[0] = req[1] = 0u;
-    rmask = 0u;
+    rmask = rkinds = 0u;
     lflags = rounds = msgs = execs = canon = dval = dtick = 0u;
-    clog = 0ull;
+    clog = 0u;
     clog_len = 0u;
     bailed = false;
   }
@@ -181,7 +182,8 @@ struct Ff1Lane {
   }
 
   // the reply of acceptor a, due next step (predicated on go)
-  __device__ __forceinline__ void reply(bool go, int a, uint32_t w, uint32_t& nmask) {
+  __device__ __forceinline__ void reply(bool go, int a, uint32_t w, uint32_t& nmask, uint32_t& nkinds) {
+    nkinds |= go ? 1u << (w >> 30) : 0u;
     bailed = bailed | (go & (((nmask >> a) & 1u) != 0u));     // (one reply per acceptor per step)
     nmask |= go ? (1u << a) : 0u;
     rsp[a] = go ? w : rsp[a];
@@ -191,7 +193,7 @@ struct Ff1Lane {
   // handleClientRequest (Server.hs:51-78) of one broadcast by every acceptor,
   // in acceptor order: one branch on the broadcast's kind, then selects (the
   // acceptors of one instance may differ: a dead one, a refused ticket)
-  __device__ __forceinline__ void accept_all(uint32_t q, uint32_t& nmask) {
+  __device__ __forceinline__ void accept_all(uint32_t q, uint32_t& nmask, uint32_t& nkinds) {
     const uint32_t kind = q >> 30, z = (q >> 28) & 3u, x = q & TM;
     const uint32_t pay = req_bytes(kind);
     if (kind == ASK) {                                        // :54-62
@@ -203,7 +205,7 @@ struct Ff1Lane {
         const bool grant = live & !(t_max >= x);              // :56
         aw[a] = grant ? (A & ~TM) | x : A;                    // :60
         // :61-62 Round1OK t prop (t, t_store, val), or :58 HaveTicket T_max
-        reply(live, a, grant ? (x | (A & (0xFFFFu << 14)) | (R1OK << 30)) : (t_max | (HAVE << 30)), nmask);
+        reply(live, a, grant ? (x | (A & (0xFFFFu << 14)) | (R1OK << 30)) : (t_max | (HAVE << 30)), nmask, nkinds);
       }
     } else if (kind == PROPOSE) {                             // :64-71
 #pragma unroll
@@ -213,7 +215,7 @@ struct Ff1Lane {
         canon += live ? 2u * pay + 32u : pay;
         const bool acc = live & (x == t_max);                 // :66 (equality, not >=)
         aw[a] = acc ? t_max | (x << 14) | (z << 28) : A;      // :68 prop := Just (t, c)
-        reply(live, a, acc ? (R2S << 30) : (t_max | (HAVE << 30)), nmask);   // :70 / :71
+        reply(live, a, acc ? (R2S << 30) : (t_max | (HAVE << 30)), nmask, nkinds);   // :70 / :71
       }
     } else {                                                  // Execute, :73-78 (no reply)
 #pragma unroll
@@ -226,12 +228,11 @@ struct Ff1Lane {
         const bool run = hit & (v != 0u);                     // :77-78 executed <>= [c]; prop := Nothing
         lflags |= panic ? (uint32_t)PXB_F_PANIC : 0u;
         aw[a] = run ? (A & TM) : (panic ? (A | (1u << 30)) : A);
-        bailed = bailed | (run & (llen[a] >= 31u));
+        bailed = bailed | (run & (llen[a] >= 16u));           // (16 positions of the 32-bit canonical log)
         accd[a] = run ? fnv_u32(accd[a], (v << 24) | 1u) : accd[a];
         const bool old = llen[a] < clog_len;
-        lflags |= (run & old & (((uint32_t)(clog >> (2u * llen[a])) & 3u) != v)) ? (uint32_t)PXB_F_LOG_DIVERGENCE
-                                                                                  : 0u;
-        clog |= (run & !old) ? (unsigned long long)v << (2u * llen[a]) : 0ull;
+        lflags |= (run & old & (((clog >> (2u * llen[a])) & 3u) != v)) ? (uint32_t)PXB_F_LOG_DIVERGENCE : 0u;
+        clog |= (run & !old) ? v << (2u * llen[a]) : 0u;
         clog_len += (run & !old) ? 1u : 0u;
         llen[a] += run ? 1u : 0u;
       }
@@ -257,9 +258,7 @@ struct Ff1Lane {
     if (rmask != 0u) {
       // the replies of one step usually share a kind (every lane of a wave in
       // the same round): one branch, then the predicated handler of that kind
-      uint32_t kinds = 0u;
-#pragma unroll
-      for (int a = 0; a < N; ++a) kinds |= ((rmask >> a) & 1u) ? 1u << (rsp[a] >> 30) : 0u;
+      const uint32_t kinds = rkinds;
       if (kinds == (1u << R1OK)) {
         bool m = false;
 #pragma unroll
@@ -292,10 +291,11 @@ struct Ff1Lane {
       }
     }
     // ---- acceptor phase: the previous step's broadcasts, in order ----
-    uint32_t nmask = 0u;
-    if (nreq > 0u) accept_all(req[0], nmask);
-    if (__builtin_expect(nreq > 1u, 0)) accept_all(req[1], nmask);
+    uint32_t nmask = 0u, nkinds = 0u;
+    if (nreq > 0u) accept_all(req[0], nmask, nkinds);
+    if (__builtin_expect(nreq > 1u, 0)) accept_all(req[1], nmask, nkinds);
     rmask = nmask;
+    rkinds = nkinds;
     nreq = nn;
     req[0] = n0;
     req[1] = n1;
