@@ -41,7 +41,7 @@ HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip
 CUS = 256
 VALU_PEAK_G = CUS * 2 * 2.4  # G wave64 VALU instructions / s (1228.8)
 PROFILES = os.path.join(ROOT, "profiles")
-BATCHES_PER_STEP = 64        # config-2 batches of 2^20 per timed step
+BATCHES_PER_STEP = 256       # config-2 batches of 2^20 per timed step (>= 100 ms over 20 steps)
 
 
 def parse():
