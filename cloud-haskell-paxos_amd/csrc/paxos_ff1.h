@@ -71,12 +71,9 @@ struct Ff1Lane {
   uint32_t aw[N], llen[N], accd[N];
   // the proposer (clientId 1): its command travels as the clientId, 1
   PropState S;
-  // in flight: the broadcasts of the previous step, the replies of the previous step
-  uint32_t nreq;                              // 0..2
-  uint32_t req[2];                            // x [13:0] | z [29:28] | kind [31:30]
-  uint32_t rmask;                             // acceptors with a reply in flight
-  uint32_t rkinds;                            // their kinds, bit 1 << kind
-  uint32_t rsp[N];                            // x [13:0] | y [27:14] | z [29:28] | kind [31:30]
+  // in flight: the broadcasts sent in the previous step (cur, handled by the
+  // acceptors now) and in this step (mid), as words x [13:0] | z [29:28] | kind [31:30]
+  uint32_t ncur, cur0, cur1, nmid, mid0, mid1;
   // per-instance outputs and counters
   uint32_t skew, lflags, rounds, msgs, execs, canon, dval, dtick;
   uint32_t clog;                              // canonical log, 2-bit values (divergence, SEMANTICS §7)
@@ -96,12 +93,27 @@ struct Ff1Lane {
       accd[a] = 0x811C9DC5u;
     }
     S = PropState{0, 0u, 0u, IDLE, 0, 0u, 0, 0u, 0u};           // Client.hs:90-95
-    nreq = req[0] = req[1] = 0u;
-    rmask = rkinds = 0u;
+    ncur = cur0 = cur1 = nmid = mid0 = mid1 = 0u;
     lflags = rounds = msgs = execs = canon = dval = dtick = 0u;
     clog = 0u;
     clog_len = 0u;
     bailed = false;
+    // step 0's proposer phase: its Tick (the replies of a step are handled
+    // within the step before, see step())
+    if (skew == 0u) tick(mid0, mid1, nmid);
+  }
+
+  // handleTick, Client.hs:196-207 (48 canonical bytes: an input of the proposer)
+  __device__ __forceinline__ void tick(uint32_t& n0, uint32_t& n1, uint32_t& nn) {
+    canon += 48u;
+    const bool t_go = S.rs == IDLE;                           // :199
+    S.ticket = t_go ? S.ticket + 1 : S.ticket;                // :200
+    S.cmd = t_go ? 1u : S.cmd;                                // :202-204 "c1.1" as clientId 1
+    S.acks = t_go ? 0u : S.acks;                              // :205
+    S.rs = t_go ? ROUND1 : S.rs;                              // :206
+    S.mr_t = t_go ? 0 : S.mr_t;
+    S.mr_v = t_go ? 0u : S.mr_v;
+    bcast(t_go, ASK, (uint32_t)S.ticket, 0u, n0, n1, nn);     // :207
   }
 
   // a broadcast of the proposer phase (Client.hs:122-123): N copies, due next
@@ -126,10 +138,7 @@ struct Ff1Lane {
   // function per reply kind, predicated on go (Q3: the sender is not checked)
   // (returns whether it reached the majority: its Propose is then the pass's
   // only broadcast, Round2 ignores further Round1OKs)
-  __device__ __forceinline__ bool fold_r1ok(bool go, int a) {
-    const uint32_t r = rsp[a];
-    const int32_t px = (int32_t)(r & TM), py = (int32_t)((r >> 14) & TM);
-    const uint32_t pz = (r >> 28) & 3u;
+  __device__ __forceinline__ bool fold_r1ok(bool go, int32_t px, int32_t py, uint32_t pz) {
     canon += go ? 2u * 16u : 0u;
     const bool o_go = go & (S.rs == ROUND1) & (S.ticket == px);        // :144-145
     const uint32_t K1 = S.acks + 1u;                                     // :146
@@ -146,8 +155,7 @@ struct Ff1Lane {
     S.mr_v = maj ? 0u : (o_go ? mv : S.mr_v);
     return maj;                                                         // :170 Propose (r2_t, r2_v)
   }
-  __device__ __forceinline__ void fold_have(bool go, int a, uint32_t& n0, uint32_t& n1, uint32_t& nn) {
-    const int32_t px = (int32_t)(rsp[a] & TM);
+  __device__ __forceinline__ void fold_have(bool go, int32_t px, uint32_t& n0, uint32_t& n1, uint32_t& nn) {
     canon += go ? 2u * 8u : 0u;
     const bool h = go & (S.rs != IDLE) & (px >= S.ticket);               // :130-132
     S.ticket = h ? px + 1 : S.ticket;                                    // :134-135
@@ -181,22 +189,28 @@ struct Ff1Lane {
     bcast(restart, ASK, t, 0u, n0, n1, nn);
   }
 
-  // the reply of acceptor a, due next step (predicated on go)
-  __device__ __forceinline__ void reply(bool go, int a, uint32_t w, uint32_t& nmask, uint32_t& nkinds) {
-    nkinds |= go ? 1u << (w >> 30) : 0u;
-    bailed = bailed | (go & (((nmask >> a) & 1u) != 0u));     // (one reply per acceptor per step)
+  // the reply of acceptor a (predicated on go): counted, at most one per
+  // acceptor per step (two would need a FIFO: bail)
+  __device__ __forceinline__ void reply(bool go, int a, uint32_t& nmask) {
+    bailed = bailed | (go & (((nmask >> a) & 1u) != 0u));
     nmask |= go ? (1u << a) : 0u;
-    rsp[a] = go ? w : rsp[a];
     msgs += go ? 1u : 0u;
   }
 
-  // handleClientRequest (Server.hs:51-78) of one broadcast by every acceptor,
-  // in acceptor order: one branch on the broadcast's kind, then selects (the
-  // acceptors of one instance may differ: a dead one, a refused ticket)
-  __device__ __forceinline__ void accept_all(uint32_t q, uint32_t& nmask, uint32_t& nkinds) {
+  // handleClientRequest (Server.hs:51-78) of broadcast q by every acceptor, in
+  // acceptor order: one branch on the broadcast's kind, then selects (the
+  // acceptors of one instance may differ: a dead one, a refused ticket).
+  // With fuse, each reply is handed straight to the proposer as an input of
+  // the next step (its proposer phase only reads the proposer state and these
+  // replies, in acceptor order, after that step's Tick): the next step's
+  // broadcasts go to n0/n1/nn.  A Round1OK / Round2Success pass issues its
+  // one broadcast after the pass unless a HaveTicket comes first.
+  __device__ __forceinline__ void accept_all(uint32_t q, bool fuse, uint32_t& nmask, uint32_t& n0, uint32_t& n1,
+                                             uint32_t& nn) {
     const uint32_t kind = q >> 30, z = (q >> 28) & 3u, x = q & TM;
     const uint32_t pay = req_bytes(kind);
     if (kind == ASK) {                                        // :54-62
+      bool m = false;
 #pragma unroll
       for (int a = 0; a < N; ++a) {
         const uint32_t A = aw[a], t_max = A & TM;
@@ -204,10 +218,18 @@ struct Ff1Lane {
         canon += live ? 2u * pay + 32u : pay;
         const bool grant = live & !(t_max >= x);              // :56
         aw[a] = grant ? (A & ~TM) | x : A;                    // :60
-        // :61-62 Round1OK t prop (t, t_store, val), or :58 HaveTicket T_max
-        reply(live, a, grant ? (x | (A & (0xFFFFu << 14)) | (R1OK << 30)) : (t_max | (HAVE << 30)), nmask, nkinds);
+        reply(live, a, nmask);
+        // :61-62 Round1OK t prop (x, t_store, val), or :58 HaveTicket T_max
+        m = m | fold_r1ok(fuse & grant, (int32_t)x, (int32_t)((A >> 14) & TM), (A >> 28) & 3u);
+        if (__builtin_expect(fuse & live & !grant, 0)) {
+          bcast(m, PROPOSE, (uint32_t)S.r2_t, S.r2_v, n0, n1, nn);
+          m = false;
+          fold_have(true, (int32_t)t_max, n0, n1, nn);
+        }
       }
+      bcast(m, PROPOSE, (uint32_t)S.r2_t, S.r2_v, n0, n1, nn);   // Client.hs:170
     } else if (kind == PROPOSE) {                             // :64-71
+      bool m = false, re = false;
 #pragma unroll
       for (int a = 0; a < N; ++a) {
         const uint32_t A = aw[a], t_max = A & TM;
@@ -215,8 +237,17 @@ struct Ff1Lane {
         canon += live ? 2u * pay + 32u : pay;
         const bool acc = live & (x == t_max);                 // :66 (equality, not >=)
         aw[a] = acc ? t_max | (x << 14) | (z << 28) : A;      // :68 prop := Just (t, c)
-        reply(live, a, acc ? (R2S << 30) : (t_max | (HAVE << 30)), nmask, nkinds);   // :70 / :71
+        reply(live, a, nmask);                                // :70 Round2Success / :71 HaveTicket T_max
+        bool r;
+        m = m | fold_r2s(fuse & acc, r);
+        re = re | r;
+        if (__builtin_expect(fuse & live & !acc, 0)) {
+          r2s_bcast(m, re, n0, n1, nn);
+          m = re = false;
+          fold_have(true, (int32_t)t_max, n0, n1, nn);
+        }
       }
+      r2s_bcast(m, re, n0, n1, nn);
     } else {                                                  // Execute, :73-78 (no reply)
 #pragma unroll
       for (int a = 0; a < N; ++a) {
@@ -239,69 +270,30 @@ struct Ff1Lane {
     }
   }
 
-  // one step (SEMANTICS §6); returns true when the instance ended after it
+  // One step s (SEMANTICS §6); returns true when the instance ended after it.
+  // Its acceptor phase handles the broadcasts sent in s - 1 and, fused with
+  // it, the proposer phase of step s + 1 runs: that step's Tick, then each
+  // reply as it is made (a reply sent in s is an input of s + 1; the proposer
+  // phase of s + 1 reads nothing else).  Below the step cap only: at s =
+  // step_cap - 1 the instance ends with those replies in flight.
   __device__ __forceinline__ bool step(uint32_t s, uint32_t step_cap, uint32_t& steps, bool& capped) {
-    // ---- proposer phase: its Tick, then the replies in acceptor order ----
-    uint32_t n0 = 0u, n1 = 0u, nn = 0u;
-    const bool tick = s == skew;
-    canon += (tick | (rmask != 0u)) ? 48u : 0u;
-    if (tick) {                                               // handleTick, Client.hs:196-207
-      const bool t_go = S.rs == IDLE;                         // :199
-      S.ticket = t_go ? S.ticket + 1 : S.ticket;              // :200
-      S.cmd = t_go ? 1u : S.cmd;                              // :202-204 "c1.1" as clientId 1
-      S.acks = t_go ? 0u : S.acks;                            // :205
-      S.rs = t_go ? ROUND1 : S.rs;                            // :206
-      S.mr_t = t_go ? 0 : S.mr_t;
-      S.mr_v = t_go ? 0u : S.mr_v;
-      bcast(t_go, ASK, (uint32_t)S.ticket, 0u, n0, n1, nn);   // :207
-    }
-    if (rmask != 0u) {
-      // the replies of one step usually share a kind (every lane of a wave in
-      // the same round): one branch, then the predicated handler of that kind
-      const uint32_t kinds = rkinds;
-      if (kinds == (1u << R1OK)) {
-        bool m = false;
-#pragma unroll
-        for (int a = 0; a < N; ++a) m = m | fold_r1ok(((rmask >> a) & 1u) != 0u, a);
-        bcast(m, PROPOSE, (uint32_t)S.r2_t, S.r2_v, n0, n1, nn);
-      } else if (kinds == (1u << R2S)) {
-        bool m = false, re = false;
-#pragma unroll
-        for (int a = 0; a < N; ++a) {
-          bool r;
-          m = m | fold_r2s(((rmask >> a) & 1u) != 0u, r);
-          re = re | r;
-        }
-        r2s_bcast(m, re, n0, n1, nn);
-      } else {
-#pragma unroll
-        for (int a = 0; a < N; ++a) {
-          const bool go = ((rmask >> a) & 1u) != 0u;
-          const uint32_t k = rsp[a] >> 30;
-          if (go & (k == R1OK)) {
-            if (fold_r1ok(true, a)) bcast(true, PROPOSE, (uint32_t)S.r2_t, S.r2_v, n0, n1, nn);
-          } else if (go & (k == HAVE)) {
-            fold_have(true, a, n0, n1, nn);
-          } else if (go) {
-            bool r;
-            const bool m = fold_r2s(true, r);
-            r2s_bcast(m, r, n0, n1, nn);
-          }
-        }
-      }
-    }
-    // ---- acceptor phase: the previous step's broadcasts, in order ----
-    uint32_t nmask = 0u, nkinds = 0u;
-    if (nreq > 0u) accept_all(req[0], nmask, nkinds);
-    if (__builtin_expect(nreq > 1u, 0)) accept_all(req[1], nmask, nkinds);
-    rmask = nmask;
-    rkinds = nkinds;
-    nreq = nn;
-    req[0] = n0;
-    req[1] = n1;
-    // ---- end of step ----
-    const bool quiet = (nreq == 0u) & (rmask == 0u) & (s >= skew);
-    capped = !quiet & (s + 1u >= step_cap);
+    const bool fuse = s + 1u < step_cap;
+    uint32_t n0 = 0u, n1 = 0u, nn = 0u;                       // the broadcasts of step s + 1
+    if (fuse & (s + 1u == skew)) tick(n0, n1, nn);
+    uint32_t nmask = 0u;
+    if (ncur > 0u) accept_all(cur0, fuse, nmask, n0, n1, nn);
+    if (__builtin_expect(ncur > 1u, 0)) accept_all(cur1, fuse, nmask, n0, n1, nn);
+    // 48 canonical bytes for the proposer's input in s + 1 (its Tick counted them)
+    canon += (fuse & (nmask != 0u) & (s + 1u != skew)) ? 48u : 0u;
+    // ---- end of step s: nothing in flight (the broadcasts of s, the replies of s) ----
+    const bool quiet = (nmid == 0u) & (nmask == 0u) & (s >= skew);
+    ncur = nmid;
+    cur0 = mid0;
+    cur1 = mid1;
+    nmid = nn;
+    mid0 = n0;
+    mid1 = n1;
+    capped = !quiet & !fuse;
     steps = s + 1u;
     return quiet | capped;
   }
@@ -326,8 +318,11 @@ struct Ff1Lane {
 // of a wave run in lockstep (every instance of a skew-free batch takes the
 // same steps).  Run totals as in the per-lane event kernel: register sums,
 // wave-reduced into one of EV_TCOPIES partial rows.
+// (N <= 5: 5 waves per SIMD, 96 VGPRs; the compiler's own choice, 101, fits 4
+// and is 5 % slower on config 2)
 template <int N>
-__global__ __launch_bounds__(256) void paxos_ff1_kernel(Ff1Params kp) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(N <= 5 ? 5 : 1))) void paxos_ff1_kernel(
+    Ff1Params kp) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   const uint32_t n_waves = gridDim.x * (blockDim.x >> 6);
