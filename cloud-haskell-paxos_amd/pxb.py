@@ -250,9 +250,31 @@ def run_multi(cfg: Config, first_instance: int, n_instances: int, n_devices: int
     return res, dig, counters_dict(tot.c)
 
 
+def _check_buf(name, t, words, itemsize):
+    """A device output buffer must be a contiguous GPU tensor of 4-byte (or, for
+    the totals, 8-byte) integers holding at least `words` elements: the kernels
+    write through its raw address."""
+    if t is None:
+        return
+    if not getattr(t, "is_cuda", False):
+        raise ValueError("%s: a CUDA (HIP) tensor is required" % name)
+    if t.element_size() != itemsize or t.dtype.is_floating_point or not t.is_contiguous():
+        raise ValueError("%s: contiguous %d-byte integer tensor required" % (name, itemsize))
+    if t.numel() < words:
+        raise ValueError("%s: %d elements, %d needed" % (name, t.numel(), words))
+
+
 def run_device(cfg: Config, first_instance: int, n_instances: int, d_results=None,
                d_digests=None, d_acceptors=None, d_totals=None, stream=None):
-    """Device-buffer, asynchronous batch run (pxb_run_device) on torch tensors."""
+    """Device-buffer, asynchronous batch run (pxb_run_device) on torch tensors
+    (sizes and dtypes checked here: the C ABI takes raw pointers)."""
+    N = cfg.n_acceptors
+    _check_buf("d_results", d_results, 4 * n_instances, 4)
+    _check_buf("d_digests", d_digests, N * n_instances, 4)
+    _check_buf("d_acceptors", d_acceptors, 4 * N * n_instances, 4)
+    if d_totals is None:
+        raise ValueError("d_totals is required")
+    _check_buf("d_totals", d_totals, NCOUNTERS, 8)
     lib = load()
     c = cfg.to_c(first_instance, n_instances)
     s = C.c_void_p(stream) if stream else None

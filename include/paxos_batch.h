@@ -135,11 +135,18 @@ int pxb_run(const pxb_config* cfg, pxb_result* out, uint32_t* log_digest,
  * NULL = default stream).  Same outputs as pxb_run but all pointers are device
  * pointers on the current device.  d_totals (PXB_NCOUNTERS int64) is ADDED to,
  * not overwritten, so many launches can accumulate into one vector.  The
- * batch runs in chunks; each chunk enqueues its kernels (faulty single-decree
- * batches: the per-lane kernel, then the general kernel over the instances it
- * handed back) and a one-block finalize kernel that folds the chunk's partial
- * totals into d_totals.  Chunks: at most 2^24 instances on the per-lane
- * kernel, 2^30 - 1 on the general faulty kernel, 2^31 fault-free.  Each chunk
+ * batch runs in chunks; each chunk enqueues its kernels and a one-block
+ * finalize kernel that folds the chunk's partial totals into d_totals:
+ *   fault-free, one proposer, single decree: the fault-free per-lane kernel,
+ *     then the general faulty kernel over the instances it handed back
+ *     (chunks of 2^30 - 1);
+ *   other fault-free: the general fault-free kernel (chunks up to 2^31);
+ *   faulty single decree: the per-lane event kernel, then the general faulty
+ *     kernel over its bailed instances; fuzzed three-proposer batches run the
+ *     two-proposer event kernel first and the three-proposer one over the
+ *     instances that drew P = 3 (chunks of 2^24);
+ *   log mode: the general kernel (chunks up to 2^30 - 1).
+ * Each chunk
  * uses one of 64 per-device scratch slots round-robin: at most 64 chunks per
  * device may be in flight at once across streams.  A launch failure after a
  * chunk's first kernel zeroes its slot (behind the queued work) before the

@@ -101,3 +101,41 @@ def test_multi_without_gpu_fails_loudly():
     lib = pxb.load()
     c = pxb.CONFIGS[3].to_c(0, 100)
     assert lib.pxb_run_multi(C.byref(c), 0, None, None, None, None) == pxb.PXB_E_NODEV
+
+
+def test_run_device_checks_buffers_before_the_abi():
+    """pxb.run_device hands raw addresses to pxb_run_device, so the Python
+    mirror checks every device buffer first: host tensors, wrong element sizes
+    and short buffers raise instead of letting a kernel write past them."""
+    import torch
+    cfg = pxb.CONFIGS[3]
+    n = 100
+    with pytest.raises(ValueError, match="CUDA"):
+        pxb.run_device(cfg, 0, n, d_totals=torch.zeros(16, dtype=torch.int64))
+    with pytest.raises(ValueError, match="required"):
+        pxb.run_device(cfg, 0, n)
+
+    class Fake:   # a stand-in for a device tensor (no GPU here)
+        def __init__(self, numel, size=4, contiguous=True):
+            self.is_cuda, self._n, self._s, self._c = True, numel, size, contiguous
+            self.dtype = torch.int32 if size == 4 else torch.int64
+
+        def element_size(self):
+            return self._s
+
+        def is_contiguous(self):
+            return self._c
+
+        def numel(self):
+            return self._n
+
+    with pytest.raises(ValueError, match="needed"):
+        pxb.run_device(cfg, 0, n, d_results=Fake(4 * n - 1), d_totals=Fake(16, 8))
+    with pytest.raises(ValueError, match="needed"):
+        pxb.run_device(cfg, 0, n, d_digests=Fake(5 * n - 1), d_totals=Fake(16, 8))
+    with pytest.raises(ValueError, match="integer"):
+        pxb.run_device(cfg, 0, n, d_results=Fake(4 * n, 8), d_totals=Fake(16, 8))
+    with pytest.raises(ValueError, match="integer"):
+        pxb.run_device(cfg, 0, n, d_results=Fake(4 * n, 4, False), d_totals=Fake(16, 8))
+    with pytest.raises(ValueError, match="needed"):
+        pxb.run_device(cfg, 0, n, d_totals=Fake(15, 8))
