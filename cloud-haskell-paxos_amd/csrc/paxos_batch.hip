@@ -517,8 +517,9 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
   // fault-free log mode: 16-bit epochs, so every block's range (static slices:
   // every wave's) stays below 2^16 instances
   // (fault-free per-lane launches: all instances alike, no tail to amortise, one launch)
-  const char* fc = getenv("PXB_FF1_CHUNK");
-  const uint64_t chunk_max = use_ff1  ? ((fc && atoi(fc) > 0) ? (1ull << atoi(fc)) : (1ull << 30) - 1)
+  // (ff1: one launch per call; A/B on config 2 at 2^26: 2^24-instance launches
+  // 2 % slower, 2^22 10 %, 2^20 33 %)
+  const uint64_t chunk_max = use_ff1  ? (1ull << 30) - 1
                              : use_ev ? std::min<uint64_t>(EV_CHUNK, (1ull << 30) - 1)
                              : (ff && logm) ? std::min<uint64_t>(resident * wpb * G * 30000ull, resident * 60000ull)
                              : ff ? std::min<uint64_t>(1ull << 31, resident * wpb * G * 30000ull)
