@@ -285,6 +285,15 @@ def test_ff1_matches_general_fault_free_kernel(gpu_lib, N):
     assert a[1]["step_cap"] > 0 and a[1]["decided"] > 0
 
 
+@pytest.mark.parametrize("cap", [1, 2, 3, 4, 5, 6, 7])
+def test_ff1_step_cap_at_every_phase(gpu_lib, cap):
+    """The fault-free per-lane kernel runs the proposer phase of step s + 1
+    inside step s; at s = step_cap - 1 it must not: caps that cut every phase
+    of the six-step round, with Tick skews 0..3, against the oracle."""
+    cfg = pxb.Config(seed=0xCA9 + cap, n_proposers=1, n_acceptors=4, skew_max=3, step_cap=cap)
+    _cmp(cfg, 99, 4000)
+
+
 def test_device_entry_accumulates_totals(gpu_lib):
     import torch
     cfg = pxb.CONFIGS[3]
