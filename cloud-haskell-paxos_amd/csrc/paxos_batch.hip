@@ -16,6 +16,7 @@
 #include "../../include/paxos_batch.h"
 #include "paxos_ev_kernel.h"
 #include "paxos_ff1.h"
+#include "paxos_ffp.h"
 #include "paxos_kernel.h"
 
 namespace pxb {
@@ -40,6 +41,10 @@ PXB_EV_FOR(PXB_EV_EXTERN, 3, 8, false) PXB_EV_FOR(PXB_EV_EXTERN, 3, 16, false) P
 #define PXB_FF1_EXTERN(N) extern template __global__ void ff1::paxos_ff1_kernel<N>(ff1::Ff1Params);
 PXB_FF1_EXTERN(2) PXB_FF1_EXTERN(3) PXB_FF1_EXTERN(4) PXB_FF1_EXTERN(5)
 PXB_FF1_EXTERN(6) PXB_FF1_EXTERN(7) PXB_FF1_EXTERN(8) PXB_FF1_EXTERN(9)
+#define PXB_FFP_EXTERN(P, N) extern template __global__ void ffp::paxos_ffp_kernel<P, N>(ffp::FfpParams);
+#define PXB_FFP_EXTERN_N(P) PXB_FFP_EXTERN(P, 2) PXB_FFP_EXTERN(P, 3) PXB_FFP_EXTERN(P, 4) PXB_FFP_EXTERN(P, 5) \
+  PXB_FFP_EXTERN(P, 6) PXB_FFP_EXTERN(P, 7) PXB_FFP_EXTERN(P, 8) PXB_FFP_EXTERN(P, 9)
+PXB_FFP_EXTERN_N(1) PXB_FFP_EXTERN_N(2) PXB_FFP_EXTERN_N(3)
 
 // ---- single-handler hook kernels ------------------------------------------
 __global__ void acceptor_hook_kernel(pxb_acceptor_rec* st, const pxb_msg* in, pxb_msg* out, uint32_t count) {
@@ -145,6 +150,25 @@ static ff1_kernel_ptr ff1_pick(uint32_t n) {
   return nullptr;
 }
 
+typedef void (*ffp_kernel_ptr)(ffp::FfpParams);
+template <int P>
+static ffp_kernel_ptr ffp_pick_n(uint32_t n) {
+  switch (n) {
+    case 2: return ffp::paxos_ffp_kernel<P, 2>;
+    case 3: return ffp::paxos_ffp_kernel<P, 3>;
+    case 4: return ffp::paxos_ffp_kernel<P, 4>;
+    case 5: return ffp::paxos_ffp_kernel<P, 5>;
+    case 6: return ffp::paxos_ffp_kernel<P, 6>;
+    case 7: return ffp::paxos_ffp_kernel<P, 7>;
+    case 8: return ffp::paxos_ffp_kernel<P, 8>;
+    case 9: return ffp::paxos_ffp_kernel<P, 9>;
+  }
+  return nullptr;
+}
+static ffp_kernel_ptr ffp_pick(uint32_t p, uint32_t n) {
+  return p == 1 ? ffp_pick_n<1>(n) : p == 2 ? ffp_pick_n<2>(n) : p == 3 ? ffp_pick_n<3>(n) : nullptr;
+}
+
 // layout index: 0 = 8-step wheel, 1 = 16-step wheel, 2 = compact links (8-step wheel)
 static ev_kernel_ptr ev_pick(uint32_t pm, uint32_t n, int layout) {
   switch (pm * 10 + (uint32_t)layout) {
@@ -236,6 +260,7 @@ static uint32_t* g_bail[64][QSLOTS];
 static uint32_t* g_split[64][QSLOTS];
 static int g_eocc[3][4][10][64];
 static int g_ff1occ[10][64];
+static int g_ffpocc[4][10][64];
 
 static int hip_fail(hipError_t e) {
   g_last_hip = (int)e;
@@ -404,10 +429,17 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
   // faulty kernel; PXB_NO_FF1=1 keeps them on the general fault-free kernel
   const char* no_ff1 = getenv("PXB_NO_FF1");
   const bool use_ff1 = ff && !logm && cfg->n_proposers == 1 && !(no_ff1 && atoi(no_ff1) > 0);
-  kernel_fn fn = pick(cfg->n_proposers, cfg->n_acceptors, logm, ff && !use_ff1);
+  // the other fault-free batches (duelling proposers, log mode) on
+  // paxos_ffp_kernel, its bails on the general faulty kernel; PXB_NO_FFP=1
+  // keeps them on the general fault-free kernel
+  const char* no_ffp = getenv("PXB_NO_FFP");
+  const bool use_ffp = ff && !use_ff1 && !(no_ffp && atoi(no_ffp) > 0);
+  kernel_fn fn = pick(cfg->n_proposers, cfg->n_acceptors, logm, ff && !use_ff1 && !use_ffp);
   if (!fn) return PXB_E_INVAL;
   const ff1_kernel_ptr ffn = use_ff1 ? ff1_pick(cfg->n_acceptors) : nullptr;
   if (use_ff1 && !ffn) return PXB_E_INVAL;
+  const ffp_kernel_ptr pfn = use_ffp ? ffp_pick(cfg->n_proposers, cfg->n_acceptors) : nullptr;
+  if (use_ffp && !pfn) return PXB_E_INVAL;
   const int layout = ev::layout_for(cfg);
   const ev_kernel_ptr efn = use_ev ? ev_pick(cfg->n_proposers, cfg->n_acceptors, layout) : nullptr;
   if (use_ev && !efn) return PXB_E_INVAL;
@@ -430,7 +462,7 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
       HIPCHK(hipGetDeviceProperties(&prop, dev));
       g_cus[dev] = prop.multiProcessorCount;
     }
-    int& o = g_occ[(logm ? 2 : 0) + ((ff && !use_ff1) ? 1 : 0)][cfg->n_proposers][cfg->n_acceptors][dev];
+    int& o = g_occ[(logm ? 2 : 0) + ((ff && !use_ff1 && !use_ffp) ? 1 : 0)][cfg->n_proposers][cfg->n_acceptors][dev];
     if (!o) {
       int nb = 0;
       HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)fn.fn, 64 * fn.wpb, 0));
@@ -457,6 +489,15 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
       if (!fo) {
         int nb = 0;
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)ffn, 256, 0));
+        fo = std::max(1, nb);
+      }
+      eocc = fo;
+    }
+    if (use_ffp) {
+      int& fo = g_ffpocc[cfg->n_proposers][cfg->n_acceptors][dev];
+      if (!fo) {
+        int nb = 0;
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)pfn, 256, 0));
         fo = std::max(1, nb);
       }
       eocc = fo;
@@ -516,10 +557,10 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
   const uint64_t wpb = (uint64_t)fn.wpb;
   // fault-free log mode: 16-bit epochs, so every block's range (static slices:
   // every wave's) stays below 2^16 instances
-  // (fault-free per-lane launches: all instances alike, no tail to amortise, one launch)
-  // (ff1: one launch per call; A/B on config 2 at 2^26: 2^24-instance launches
-  // 2 % slower, 2^22 10 %, 2^20 33 %)
-  const uint64_t chunk_max = use_ff1  ? (1ull << 30) - 1
+  // fault-free per-lane kernels: as few launches as the general faulty kernel
+  // allows (it may have to re-run a whole chunk); A/B on config 2 at 2^26:
+  // 2^24-instance launches 2 % slower, 2^22 10 %, 2^20 33 %
+  const uint64_t chunk_max = (use_ff1 || use_ffp) ? std::min<uint64_t>((1ull << 30) - 1, resident * wpb * G * 60000ull)
                              : use_ev ? std::min<uint64_t>(EV_CHUNK, (1ull << 30) - 1)
                              : (ff && logm) ? std::min<uint64_t>(resident * wpb * G * 30000ull, resident * 60000ull)
                              : ff ? std::min<uint64_t>(1ull << 31, resident * wpb * G * 30000ull)
@@ -539,7 +580,7 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
       slot = g_slots[dev] + (size_t)sidx * SLOT_U64;
       kp.part = slot;
       kp.queue = reinterpret_cast<uint32_t*>(slot + 2 * ROWS_U64);
-      if (use_ev || use_ff1) {
+      if (use_ev || use_ff1 || use_ffp) {
         if (!g_bail[dev][sidx]) HIPCHK(hipMalloc(&g_bail[dev][sidx], (size_t)EV_BAIL_CAP * sizeof(uint32_t)));
         bail = g_bail[dev][sidx];
       }
@@ -577,6 +618,38 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
       const uint64_t fres = (uint64_t)eocc * (uint64_t)cus;
       const unsigned fgrid = (unsigned)std::min<uint64_t>((nc + 255) / 256, fres);
       hipLaunchKernelGGL(ffn, dim3(fgrid), dim3(256), 0, st, fp);
+      HIPCHK(hipGetLastError());
+      kp.ids = bail;
+      kp.n_ids = kp.queue + Q_BAIL;
+      kp.ids_cap = bail_cap;
+      hipLaunchKernelGGL(fn.fn, dim3((unsigned)resident), dim3(64 * fn.wpb), 0, st, kp);
+      if (hipError_t e = hipGetLastError()) return fail(e);
+    } else if (use_ffp) {
+      // the fault-free per-lane kernel for duelling proposers / log mode, then
+      // the general faulty kernel over its bailed ids
+      ffp::FfpParams fp;
+      memset(&fp, 0, sizeof(fp));
+      fp.first_instance = kp.first_instance;
+      fp.k0 = kp.k0;
+      fp.k1 = kp.k1;
+      fp.n_prop = cfg->n_proposers;
+      fp.skew_max = cfg->skew_max;
+      fp.step_cap = cfg->step_cap;
+      fp.n_ticks = kp.n_ticks;
+      fp.tick_period = kp.tick_period;
+      fp.n_instances = (uint32_t)nc;
+      fp.out = kp.out;
+      fp.dig = kp.dig;
+      fp.acc = kp.acc;
+      fp.part = kp.part + ROWS_U64;
+      fp.bail_ids = bail;
+      fp.bail_n = kp.queue + Q_BAIL;
+      fp.bail_cap = bail_cap;
+      const char* fb = getenv("PXB_FF1_BAIL");           // tests: hand every instance to the general kernel
+      fp.bail_all = (fb && atoi(fb) > 0) ? 1u : 0u;
+      const uint64_t fres = (uint64_t)eocc * (uint64_t)cus;
+      const unsigned fgrid = (unsigned)std::min<uint64_t>((nc + 255) / 256, fres);
+      hipLaunchKernelGGL(pfn, dim3(fgrid), dim3(256), 0, st, fp);
       HIPCHK(hipGetLastError());
       kp.ids = bail;
       kp.n_ids = kp.queue + Q_BAIL;

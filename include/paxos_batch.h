@@ -139,13 +139,14 @@ int pxb_run(const pxb_config* cfg, pxb_result* out, uint32_t* log_digest,
  * finalize kernel that folds the chunk's partial totals into d_totals:
  *   fault-free, one proposer, single decree: the fault-free per-lane kernel,
  *     then the general faulty kernel over the instances it handed back
- *     (chunks of 2^30 - 1);
- *   other fault-free: the general fault-free kernel (chunks up to 2^31);
+ *     (chunks up to 2^30 - 1);
+ *   other fault-free (duelling proposers, log mode): the fault-free per-lane
+ *     kernel for those, then the general faulty kernel over its bails;
  *   faulty single decree: the per-lane event kernel, then the general faulty
  *     kernel over its bailed instances; fuzzed three-proposer batches run the
  *     two-proposer event kernel first and the three-proposer one over the
  *     instances that drew P = 3 (chunks of 2^24);
- *   log mode: the general kernel (chunks up to 2^30 - 1).
+ *   faulty log mode: the general kernel (chunks up to 2^30 - 1).
  * Each chunk
  * uses one of 64 per-device scratch slots round-robin: at most 64 chunks per
  * device may be in flight at once across streams.  A launch failure after a

@@ -285,6 +285,26 @@ def test_ff1_matches_general_fault_free_kernel(gpu_lib, N):
     assert a[1]["step_cap"] > 0 and a[1]["decided"] > 0
 
 
+@pytest.mark.parametrize("P,N,ticks,period,skew,cap", [
+    (2, 2, 16, 8, 0, 1024), (2, 5, 1, 1, 2, 600), (3, 9, 1, 1, 3, 300), (1, 3, 40, 2, 1, 1024),
+    (3, 4, 6, 3, 2, 64), (2, 7, 5, 7, 4, 9)])
+def test_ffp_matches_general_fault_free_kernel(gpu_lib, P, N, ticks, period, skew, cap):
+    """Duelling / log-mode fault-free batches on their per-lane kernel
+    (paxos_ffp.h) against the oracle and the general fault-free kernel
+    (PXB_NO_FFP=1), logs past PXB_LOG_TRACK and step caps included; and with
+    every instance handed to the general faulty kernel (PXB_FF1_BAIL=1)."""
+    cfg = pxb.Config(seed=0xFF9 + 16 * P + N, n_proposers=P, n_acceptors=N, skew_max=skew, step_cap=cap,
+                     n_ticks=ticks, tick_period=period)
+    a = _cmp(cfg, (1 << 32) - 1500, 3000)
+    for env in ("PXB_NO_FFP", "PXB_FF1_BAIL"):
+        os.environ[env] = "1"
+        try:
+            b = _cmp(cfg, (1 << 32) - 1500, 3000)
+        finally:
+            del os.environ[env]
+        assert np.array_equal(a[0], b[0]) and a[1] == b[1], env
+
+
 @pytest.mark.parametrize("cap", [1, 2, 3, 4, 5, 6, 7])
 def test_ff1_step_cap_at_every_phase(gpu_lib, cap):
     """The fault-free per-lane kernel runs the proposer phase of step s + 1
