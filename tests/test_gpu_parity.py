@@ -501,6 +501,21 @@ def test_random_schedules_match_oracle(gpu_lib, i):
     _cmp(cfg, int(rng.integers(0, 1 << 34)), int(rng.integers(1, 1500)))
 
 
+@pytest.mark.parametrize("i", range(24))
+def test_random_fault_free_schedules_match_oracle(gpu_lib, i):
+    """24 seeded fault-free draws (the per-lane fault-free kernels: one or more
+    proposers, Tick skew, step caps, single decree or log mode with up to 40
+    Ticks): everything equals the oracle's."""
+    rng = np.random.default_rng(0xFF0 + i)
+    log = rng.random() < 0.5
+    cfg = pxb.Config(seed=int(rng.integers(0, 1 << 63)), n_proposers=int(rng.integers(1, 4)),
+                     n_acceptors=int(rng.integers(2, 10)), skew_max=int(rng.choice([0, rng.integers(1, 12)])),
+                     step_cap=int(rng.choice([int(rng.integers(1, 40)), 256, 1024])),
+                     n_ticks=int(rng.integers(2, 41)) if log else 1,
+                     tick_period=int(rng.integers(1, 12)) if log else 1)
+    _cmp(cfg, int(rng.integers(0, 1 << 34)), int(rng.integers(1, 2500)))
+
+
 # ---- per-instance trace (pxb_trace_instance; Server.hs:85 / Client.hs:108) ----
 def _oracle_trace(cfg, inst):
     import paxos_ref as R
