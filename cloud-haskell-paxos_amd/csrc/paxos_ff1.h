@@ -209,27 +209,68 @@ struct Ff1Lane {
                                              uint32_t& nn) {
     const uint32_t kind = q >> 30, z = (q >> 28) & 3u, x = q & TM;
     const uint32_t pay = req_bytes(kind);
+    constexpr uint32_t MAJ = (uint32_t)N >> 1;               // haveMajority: acks > floor(N/2), Client.hs:191-194
     if (kind == ASK) {                                        // :54-62
-      bool m = false;
+      uint32_t G = 0u, L = 0u;                                // granting / live acceptors
 #pragma unroll
       for (int a = 0; a < N; ++a) {
         const uint32_t A = aw[a], t_max = A & TM;
         const bool live = (A >> 30) == 0u;
         canon += live ? 2u * pay + 32u : pay;
         const bool grant = live & !(t_max >= x);              // :56
-        aw[a] = grant ? (A & ~TM) | x : A;                    // :60
-        reply(live, a, nmask);
-        // :61-62 Round1OK t prop (x, t_store, val), or :58 HaveTicket T_max
-        m = m | fold_r1ok(fuse & grant, (int32_t)x, (int32_t)((A >> 14) & TM), (A >> 28) & 3u);
-        if (__builtin_expect(fuse & live & !grant, 0)) {
+        aw[a] = grant ? (A & ~TM) | x : A;                    // :60 (t_store, val unchanged)
+        reply(live, a, nmask);                                // :61-62 Round1OK t prop / :58 HaveTicket T_max
+        G |= grant ? 1u << a : 0u;
+        L |= live ? 1u << a : 0u;
+      }
+      if (fuse & (L != 0u)) {
+        if (__builtin_expect(L == G, 1)) {
+          // only Round1OKs (Client.hs:142-170), in acceptor order: while in
+          // Round1 at ticket x each one counts, up to the majority, folding its
+          // proposal into mr (Common.hs:61-65); after it, Round2 ignores them
+          canon += 2u * 16u * (uint32_t)__builtin_popcount(G);
+          const bool o_go = (S.rs == ROUND1) & (S.ticket == (int32_t)x);
+          const uint32_t need = MAJ + 1u - S.acks, cnt = (uint32_t)__builtin_popcount(G);
+          const bool maj = o_go & (cnt >= need);
+          int32_t mt = S.mr_t;
+          uint32_t mv = S.mr_v, seen = 0u;
+#pragma unroll
+          for (int a = 0; a < N; ++a) {
+            const bool g = (((G >> a) & 1u) != 0u) & (seen < need);
+            seen += ((G >> a) & 1u);
+            const int32_t py = (int32_t)((aw[a] >> 14) & TM);
+            const uint32_t pz = (aw[a] >> 28) & 3u;
+            const bool take = g & ((mv == 0u) | ((pz != 0u) & !(mt >= py)));
+            mt = take ? py : mt;
+            mv = take ? pz : mv;
+          }
+          S.r2_t = maj ? (int32_t)x : S.r2_t;                 // :157-167 (Q5: pending whenever mr is Just)
+          S.r2_v = maj ? ((mv == 0u) ? S.cmd : mv) : S.r2_v;
+          S.pending = maj ? ((mv != 0u) ? 1u : 0u) : S.pending;
+          S.acks = maj ? 0u : (o_go ? S.acks + cnt : S.acks);   // :146 / :168
+          S.rs = maj ? ROUND2 : S.rs;                          // :169
+          S.mr_t = maj ? 0 : (o_go ? mt : S.mr_t);
+          S.mr_v = maj ? 0u : (o_go ? mv : S.mr_v);
+          bcast(maj, PROPOSE, x, S.r2_v, n0, n1, nn);          // :170
+        } else {
+          // a HaveTicket among them: every reply through its handler, in order
+          bool m = false;
+#pragma unroll
+          for (int a = 0; a < N; ++a) {
+            const uint32_t A = aw[a];
+            if ((G >> a) & 1u) {
+              m = m | fold_r1ok(true, (int32_t)x, (int32_t)((A >> 14) & TM), (A >> 28) & 3u);
+            } else if ((L >> a) & 1u) {
+              bcast(m, PROPOSE, (uint32_t)S.r2_t, S.r2_v, n0, n1, nn);
+              m = false;
+              fold_have(true, (int32_t)(A & TM), n0, n1, nn);
+            }
+          }
           bcast(m, PROPOSE, (uint32_t)S.r2_t, S.r2_v, n0, n1, nn);
-          m = false;
-          fold_have(true, (int32_t)t_max, n0, n1, nn);
         }
       }
-      bcast(m, PROPOSE, (uint32_t)S.r2_t, S.r2_v, n0, n1, nn);   // Client.hs:170
     } else if (kind == PROPOSE) {                             // :64-71
-      bool m = false, re = false;
+      uint32_t G = 0u, L = 0u;                                // accepting / live acceptors
 #pragma unroll
       for (int a = 0; a < N; ++a) {
         const uint32_t A = aw[a], t_max = A & TM;
@@ -238,16 +279,42 @@ struct Ff1Lane {
         const bool acc = live & (x == t_max);                 // :66 (equality, not >=)
         aw[a] = acc ? t_max | (x << 14) | (z << 28) : A;      // :68 prop := Just (t, c)
         reply(live, a, nmask);                                // :70 Round2Success / :71 HaveTicket T_max
-        bool r;
-        m = m | fold_r2s(fuse & acc, r);
-        re = re | r;
-        if (__builtin_expect(fuse & live & !acc, 0)) {
+        G |= acc ? 1u << a : 0u;
+        L |= live ? 1u << a : 0u;
+      }
+      if (fuse & (L != 0u)) {
+        if (__builtin_expect(L == G, 1)) {
+          // only Round2Successes (Client.hs:172-189): in Round2 each counts (no
+          // ticket: Q2) up to the majority; then Idle or, pending, Round1 ignore them
+          canon += 2u * 4u * (uint32_t)__builtin_popcount(G);
+          const bool s_go = S.rs == ROUND2;
+          const uint32_t need = MAJ + 1u - S.acks, cnt = (uint32_t)__builtin_popcount(G);
+          const bool maj = s_go & (cnt >= need);
+          const bool restart = maj & (S.pending != 0u);       // :179
+          S.ticket = restart ? S.ticket + 1 : S.ticket;       // :182
+          S.acks = maj ? 0u : (s_go ? S.acks + cnt : S.acks); // :175 / :183 / :188
+          S.rs = restart ? ROUND1 : (maj ? IDLE : S.rs);      // :184 / :189
+          S.mr_t = restart ? 0 : S.mr_t;
+          S.mr_v = restart ? 0u : S.mr_v;
+          S.cmd = (maj & !restart) ? 0u : S.cmd;              // :187
+          r2s_bcast(maj, restart, n0, n1, nn);                // :178 Execute, :185 AskForTicket
+        } else {
+          bool m = false, re = false;
+#pragma unroll
+          for (int a = 0; a < N; ++a) {
+            if ((G >> a) & 1u) {
+              bool r;
+              m = m | fold_r2s(true, r);
+              re = re | r;
+            } else if ((L >> a) & 1u) {
+              r2s_bcast(m, re, n0, n1, nn);
+              m = re = false;
+              fold_have(true, (int32_t)(aw[a] & TM), n0, n1, nn);
+            }
+          }
           r2s_bcast(m, re, n0, n1, nn);
-          m = re = false;
-          fold_have(true, (int32_t)t_max, n0, n1, nn);
         }
       }
-      r2s_bcast(m, re, n0, n1, nn);
     } else {                                                  // Execute, :73-78 (no reply)
 #pragma unroll
       for (int a = 0; a < N; ++a) {
@@ -321,7 +388,10 @@ struct Ff1Lane {
 // (N <= 5: 5 waves per SIMD, 96 VGPRs; the compiler's own choice, 101, fits 4
 // and is 5 % slower on config 2)
 template <int N>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(N <= 5 ? 5 : 1))) void paxos_ff1_kernel(
+#ifndef PXB_FF1_W5
+#define PXB_FF1_W5 5
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(N <= 5 ? PXB_FF1_W5 : 1))) void paxos_ff1_kernel(
     Ff1Params kp) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
