@@ -248,14 +248,17 @@ static uint32_t g_qseq[64];
 // (BASELINE configs: <= 1.5 %); a chunk whose list overflows is re-run whole
 // by the general kernel (finalize_kernel then drops the per-lane totals).
 // Big chunks matter: each one ends with a tail (the slowest instances of the
-// last waves, then of the bailed ones on the general kernel).
-constexpr uint64_t EV_CHUNK = 1ull << 24;
-constexpr uint32_t EV_BAIL_CAP = 1u << 20;
+// last waves, then of the bailed ones on the general kernel); config 4 at 2^26
+// on one GPU: 2^24-instance chunks 1292.6 ms, 2^25 1283.8, 2^26 1277.3.  The
+// list holds 1/16 of a chunk (16 MB per slot).
+constexpr uint64_t EV_CHUNK = 1ull << 26;
+constexpr uint32_t EV_BAIL_CAP = 1u << 22;
 // split routing (fuzzed P = 3 batches, config 5): the per-lane kernel of a
 // two-proposer shape takes the instances that drew P <= 2 and lists the P = 3
 // ones (a third) with its bails for the three-proposer shape, so that list
-// holds half a chunk
-constexpr uint32_t EV_SPLIT_CAP = (uint32_t)(EV_CHUNK / 2);
+// holds half a chunk; split chunks are 2^24 instances (32 MB lists)
+constexpr uint64_t EV_SPLIT_CHUNK = 1ull << 24;
+constexpr uint32_t EV_SPLIT_CAP = (uint32_t)(EV_SPLIT_CHUNK / 2);
 static uint32_t* g_bail[64][QSLOTS];
 static uint32_t* g_split[64][QSLOTS];
 static int g_eocc[3][4][10][64];
@@ -557,11 +560,12 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
   const uint64_t wpb = (uint64_t)fn.wpb;
   // fault-free log mode: 16-bit epochs, so every block's range (static slices:
   // every wave's) stays below 2^16 instances
+  const uint64_t ev_chunk = split ? EV_SPLIT_CHUNK : EV_CHUNK;
   // fault-free per-lane kernels: as few launches as the general faulty kernel
   // allows (it may have to re-run a whole chunk); A/B on config 2 at 2^26:
   // 2^24-instance launches 2 % slower, 2^22 10 %, 2^20 33 %
   const uint64_t chunk_max = (use_ff1 || use_ffp) ? std::min<uint64_t>((1ull << 30) - 1, resident * wpb * G * 60000ull)
-                             : use_ev ? std::min<uint64_t>(EV_CHUNK, (1ull << 30) - 1)
+                             : use_ev ? ev_chunk
                              : (ff && logm) ? std::min<uint64_t>(resident * wpb * G * 30000ull, resident * 60000ull)
                              : ff ? std::min<uint64_t>(1ull << 31, resident * wpb * G * 30000ull)
                                   : std::min<uint64_t>((1ull << 30) - 1, resident * wpb * G * 60000ull);
