@@ -196,6 +196,27 @@ def test_config5_per_gpu_share_sampled(gpu_lib):
         assert np.array_equal(res[i], eres[0]) and np.array_equal(dig[i], edig[0])
 
 
+def test_config4_north_star_full_size_sampled(gpu_lib):
+    """The north star at its size on one GPU: BASELINE config 4, 2^26
+    instances in one call (one per-lane chunk, its bailed instances on the
+    general kernel): totals equal the per-instance flags and 64 random
+    instances match the oracle bit-exact."""
+    cfg = pxb.CONFIGS[4]
+    n = 1 << 26
+    res, dig, _, cnt = pxb.run(cfg, 0, n)
+    assert cnt["instances"] == n and cnt["decided"] + cnt["undecided"] == n
+    flags = res[:, 3] & 0xFF
+    for key, bit in (("undecided", pxb.F_UNDECIDED), ("stuck", pxb.F_STUCK), ("panic", pxb.F_PANIC),
+                     ("divergence", pxb.F_LOG_DIVERGENCE), ("step_cap", pxb.F_STEP_CAP)):
+        assert cnt[key] == int(((flags & bit) != 0).sum()), key
+    assert cnt["rounds"] == int(res[:, 2].astype(np.int64).sum())
+    assert cnt["steps"] == int((res[:, 3] >> 16).astype(np.int64).sum())
+    rng = np.random.default_rng(44)
+    for i in rng.choice(n, 64, replace=False):
+        eres, edig, _, _ = oracle_c.run_cpu(cfg, int(i), 1)
+        assert np.array_equal(res[i], eres[0]) and np.array_equal(dig[i], edig[0])
+
+
 @pytest.mark.parametrize("cap", [0, 3, 1 << 20])
 def test_per_lane_bail_list_overflow(gpu_lib, cap):
     """Instances the per-lane kernel cannot hold go to a capped id list for the
