@@ -531,6 +531,19 @@ struct EvLane {
   // known before the acceptor part, which does not touch the pending queue).
   __host__ __device__ __forceinline__ bool step(const EvParams& kp, EvOut& o) {
     Reply rp;
+    if constexpr (!CMP) {
+      // 4-entry layouts (fewer resident waves: config 5 runs 4-6 per CU): the
+      // proposer input first, so its link and pool loads start the iteration
+      // instead of waiting behind the acceptor op; a pop and an append on one
+      // FIFO commute (bails may differ, and stay exact).  Config 5 +2.3 %; the
+      // compact layout (10 waves per CU) keeps the order below.
+      prop_op(kp, true);
+      const uint4 w0 = acc_op(kp, true, copy_ctr(), rp);
+      send_first(kp, w0, rp);
+      const uint2 c = copy_ctr();
+      copy_send(kp, true, draw(c.x, c.y));
+      return end_op(kp, o, true);
+    }
     const uint4 w0 = acc_op(kp, true, copy_ctr(), rp);
     send_first(kp, w0, rp);
     prop_op(kp, true);
