@@ -535,7 +535,8 @@ struct EvLane {
     // on one FIFO commute (bails may differ, and stay exact).  MI355X, 2^24
     // instances: config 3 +2.7 %, config 4 +1.3 %, config 5 +2.3 %.
     // The copy's counter is then known at the start too, so its Philox chain
-    // overlaps the acceptor op (config 4 +1.7 %, config 3 +0.7 %, config 5 +0.9 %).
+    // overlaps the acceptor op (config 4 +1.7 %, config 3 +0.7 %, config 5 +0.9 %);
+    // the copy before the proposer op measured 1-3 % slower.
     Reply rp;
     prop_op(kp, true);
     const uint2 c = copy_ctr();
