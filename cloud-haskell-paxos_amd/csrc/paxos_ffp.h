@@ -327,8 +327,18 @@ struct FfpLane {
 // Grid-stride over the launch's instances, one per lane at a time (as
 // paxos_ff1_kernel); run totals in registers, wave-reduced into one of
 // EV_TCOPIES partial rows (plus the log-truncation count).
+// Waves per SIMD the register allocation targets (1 = the compiler's choice):
+// the stock Main.hs log-mode workload, P = 2 and N = 2, at 6 (1.55 -> 1.73 G
+// instances/s on MI355X); one proposer over five acceptors with 8 Ticks at 5
+// (3.35 -> 3.59 G/s); the other small shapes where that spills at most a few
+// words (one proposer, N <= 3: 6)
 template <int PM, int N>
-__global__ __launch_bounds__(256) void paxos_ffp_kernel(FfpParams kp) {
+constexpr int ffp_waves() {
+  return (PM == 2 && N == 2) ? 6 : (PM == 1 && N <= 3) ? 6 : (PM == 1 && N == 5) ? 5 : 1;
+}
+template <int PM, int N>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ffp_waves<PM, N>())))
+void paxos_ffp_kernel(FfpParams kp) {
   __shared__ uint32_t s_clog[4][LT / 2][64];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wib = threadIdx.x >> 6;
