@@ -145,7 +145,7 @@ int pxb_run(const pxb_config* cfg, pxb_result* out, uint32_t* log_digest,
  *   faulty single decree: the per-lane event kernel, then the general faulty
  *     kernel over its bailed instances; fuzzed three-proposer batches run the
  *     two-proposer event kernel first and the three-proposer one over the
- *     instances that drew P = 3 (chunks of 2^26; 2^24 split);
+ *     instances that drew P = 3 (chunks of 2^26; 2^25 split);
  *   faulty log mode: the general kernel (chunks up to 2^30 - 1).
  * Each chunk
  * uses one of 64 per-device scratch slots round-robin: at most 64 chunks per
