@@ -5,8 +5,8 @@
 One step = one pxb_run_device call over one batch of fresh synthetic
 instances.  The headline workload is BASELINE config 2 (1 proposer, 5
 acceptors, no faults; the single-GPU configuration the metric is quoted on):
-a step runs 64 config-2 batches of 2^20 instances (2^26 fresh global ids), so
-the default 20 steps time well over 100 ms.  Instances are generated on the
+a step runs BATCHES_PER_STEP = 256 config-2 batches of 2^20 instances (2^28
+fresh global ids), so the default 20 steps time well over 100 ms.  Instances are generated on the
 device from (seed, global instance id), so the inputs are resident before the
 timed region; outputs (16 B result + 4 B/acceptor digest per instance) are
 written to HBM.
@@ -18,9 +18,12 @@ without torchrun spawns the N ranks itself (a child torch.distributed.run,
 started before this process touches a GPU).  Prints ONE JSON line on rank 0.
 
 The line also carries the north-star workload (BASELINE config 4: 64M
-instances with seeded crash windows, on this one GPU) with its own roofline,
-the other faulty configs at scale, and the CPU baseline (the oracle's C port
-on the host cores).
+instances with seeded crash windows) with its own roofline: 2^26 instances
+split over the N ranks (strong scaling, 2^26 / N per GPU, barriers and the
+max-over-ranks time as above, totals all-reduced over RCCL).  On one GPU it
+also carries config 4 at 2^23 (the per-GPU share at N = 8), the other faulty
+configs at scale, log mode, and the CPU baseline (the oracle's C port on the
+host cores).
 """
 from __future__ import annotations
 
@@ -42,6 +45,7 @@ CUS = 256
 VALU_PEAK_G = CUS * 2 * 2.4  # G wave64 VALU instructions / s (1228.8)
 PROFILES = os.path.join(ROOT, "profiles")
 BATCHES_PER_STEP = 256       # config-2 batches of 2^20 per timed step (>= 100 ms over 20 steps)
+DRY_NORTH_STAR = 1 << 12     # --dry-run stand-in for the north star's 2^26 total
 
 
 def parse():
@@ -70,16 +74,22 @@ def spawn_ranks(args) -> int:
     return subprocess.call(cmd)
 
 
-def step_instances(c: int, override: int) -> int:
-    """Instances per GPU per step."""
+def step_instances(c: int, override: int, world: int = 1) -> int:
+    """Instances per GPU per step.  Config 2 is weak-scaled (a fixed batch per
+    GPU); configs 4 and 5 are quoted as one batch over the node (64M over 8
+    GPUs, 256M), so each rank runs its 1/world share of that batch."""
     import pxb
     if override:
         return override
     if c == 2:
         return BATCHES_PER_STEP * pxb.CONFIG_INSTANCES[2]
     if c in (4, 5):
-        return pxb.CONFIG_INSTANCES[c] // 8        # quoted over 8 GPUs: the per-GPU share
+        return pxb.CONFIG_INSTANCES[c] // world
     return pxb.CONFIG_INSTANCES[c]
+
+
+def scaling_of(c: int) -> str:
+    return "strong" if c in (4, 5) else "weak"
 
 
 class GpuLeg:
@@ -323,15 +333,36 @@ def cpu_baseline(cfg, budget_s):
             "one_core": {"value": one / dt1, "sample": "%d further instances, 1 thread, %.1f s" % (one, dt1)}}
 
 
-def faulty_line(name, c, n, steps, warmup, stream, dev, warm_n):
+def faulty_line(name, c, n, steps, warmup, stream, dev, warm_n, rank=0, world=1, leg=None):
+    """One faulty workload: n instances per rank per step, on every rank of the
+    job (barriers, max-over-ranks time, all-reduced totals: run_workload)."""
     import pxb
-    es, ek, ecnt = run_workload(GpuLeg(pxb.CONFIGS[c], n, 0, 1, stream, dev), n, steps, warmup, 1, warm_n=warm_n)
-    line = {"workload": name, "instances_per_step": n, "instances_per_s": ecnt["instances"] / es,
-            "decided_per_s": ecnt["decided"] / es, "ms_per_step": es / steps * 1e3, "kernel_ms": ek,
-            "mean_steps_per_instance": ecnt["steps"] / max(1, ecnt["instances"]),
-            "roofline": roofline("config%d" % c, n, ek, ecnt["canon_bytes"] / steps), "counters": ecnt}
-    assert ecnt["instances"] == n * steps, ecnt
+    leg = leg or GpuLeg(pxb.CONFIGS[c], n, rank, world, stream, dev)
+    es, ek, ecnt = run_workload(leg, n, steps, warmup, world, warm_n=warm_n)
+    line = {"workload": name, "instances_per_step": n * world, "instances_per_gpu_per_step": n, "n_gpus": world,
+            "instances_per_s": ecnt["instances"] / es, "decided_per_s": ecnt["decided"] / es,
+            "ms_per_step": es / steps * 1e3, "kernel_ms": ek,
+            "mean_steps_per_instance": ecnt["steps"] / max(1, ecnt["instances"]), "counters": ecnt}
+    if leg.__class__ is GpuLeg:
+        line["roofline"] = roofline("config%d" % c, n, ek, ecnt["canon_bytes"] / (steps * world))
+    assert ecnt["instances"] == n * steps * world, ecnt
     assert ecnt["decided"] + ecnt["undecided"] == ecnt["instances"]
+    return line
+
+
+def north_star_line(rank, world, stream=None, dev=None, dry_total=0):
+    """BASELINE config 4 as the north star states it: 2^26 instances with
+    seeded crash windows sharded over the node's GPUs (2^26 / world per rank,
+    contiguous global-id ranges), strong scaling.  Every rank runs it."""
+    import pxb
+    total = dry_total or pxb.CONFIG_INSTANCES[4]
+    n = total // world
+    leg = DryLeg(n, rank, world) if dry_total else None
+    line = faulty_line("BASELINE config 4: 2^%d instances over %d GPU%s (%d per GPU)" % (
+                           total.bit_length() - 1, world, "s" if world > 1 else "", n),
+                       4, n, 1, 1, stream, dev, min(n, 1 << 22), rank=rank, world=world, leg=leg)
+    line["scaling"] = "strong"
+    line["rccl_world"] = world
     return line
 
 
@@ -344,10 +375,14 @@ def dry_main(args, rank, world):
     n = args.instances or 1000
     secs, kms, cnt = run_workload(DryLeg(n, rank, world), n, args.steps, args.warmup, world)
     assert cnt["instances"] == n * world * args.steps, cnt
+    ns = None if args.no_extra else north_star_line(rank, world, dry_total=DRY_NORTH_STAR)
     if rank == 0:
-        print(json.dumps({"metric": "dry-run", "value": cnt["decided"] / secs, "n_gpus": world, "steps": args.steps,
-                          "warmup": args.warmup, "ms_per_step": secs / args.steps * 1e3, "data": "dry-run",
-                          "rccl_world": world, "counters": cnt}), flush=True)
+        line = {"metric": "dry-run", "value": cnt["decided"] / secs, "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": secs / args.steps * 1e3, "data": "dry-run",
+                "rccl_world": world, "counters": cnt}
+        if ns:
+            line["north_star"] = ns
+        print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -373,7 +408,7 @@ def main():
     stream = torch.cuda.Stream(dev)
     c = args.config
     cfg = pxb.CONFIGS[c]
-    n = step_instances(c, args.instances)
+    n = step_instances(c, args.instances, world)
 
     secs, kms, cnt = run_workload(GpuLeg(cfg, n, rank, world, stream, dev), n, args.steps, args.warmup, world)
     total_inst = n * world * args.steps
@@ -390,7 +425,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": secs / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling_of(c),
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic (Philox4x32-10 schedule from seed + global instance id)",
@@ -405,12 +440,17 @@ def main():
         "roofline": roofline("config%d" % c, n, kms, cnt["canon_bytes"] / (args.steps * world)),
         "counters": cnt,
     }
-    if rank == 0 and not args.no_extra and c == 2 and world == 1:
+    if not args.no_extra and c == 2:
         # the north star: BASELINE config 4 (64M instances, 2 duelling proposers,
-        # 7 acceptors, seeded crash windows) all on this one GPU
-        line["north_star"] = faulty_line("BASELINE config 4: 2^26 instances on 1 GPU", 4,
-                                         pxb.CONFIG_INSTANCES[4], 1, 1, stream, dev, 1 << 22)
+        # 7 acceptors, seeded crash windows) over this job's GPUs, every rank
+        line["north_star"] = north_star_line(rank, world, stream, dev)
+    if rank == 0 and not args.no_extra and c == 2 and world == 1:
         extra = {}
+        # config 4 at its per-GPU share at N = 8 (2^23): the chunk-tail cost at
+        # that size, before any 8-GPU run
+        extra["config4_share"] = faulty_line("BASELINE config 4: 2^23 instances (the per-GPU share of 2^26 "
+                                             "over 8 GPUs) on 1 GPU", 4, pxb.CONFIG_INSTANCES[4] // 8, 2, 1,
+                                             stream, dev, 1 << 22)
         extra["config3"] = faulty_line("BASELINE config 3: 2^24 instances", 3, pxb.CONFIG_INSTANCES[3],
                                        2, 1, stream, dev, 1 << 22)
         extra["config5"] = faulty_line("BASELINE config 5: 2^25 instances (the per-GPU share of 2^28 "

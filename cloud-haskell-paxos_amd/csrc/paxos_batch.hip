@@ -243,8 +243,9 @@ constexpr size_t ROWS_U64 = (size_t)TCOPIES * 16;
 constexpr size_t SLOT_U64 = 2 * ROWS_U64 + 16;
 static unsigned long long* g_slots[64];
 static uint32_t g_qseq[64];
-// Per-lane kernel: one launch per EV_CHUNK instances; its bailed ids go to the
-// slot's list of EV_BAIL_CAP entries (lazily allocated).  Bails are rare
+// Per-lane kernel: one launch per EV_CHUNK instances; its bailed ids go to a
+// list of EV_BAIL_CAP entries (16 MB) kept per (device, stream): launches of
+// one stream run in order, so they can share it.  Bails are rare
 // (BASELINE configs: <= 1.5 %); a chunk whose list overflows is re-run whole
 // by the general kernel (finalize_kernel then drops the per-lane totals).
 // Big chunks matter: each one ends with a tail (the slowest instances of the
@@ -261,8 +262,17 @@ constexpr uint32_t EV_BAIL_CAP = 1u << 22;
 // chunks, 36.2 with 2^25)
 constexpr uint64_t EV_SPLIT_CHUNK = 1ull << 25;
 constexpr uint32_t EV_SPLIT_CAP = (uint32_t)(EV_SPLIT_CHUNK / 2);
-static uint32_t* g_bail[64][QSLOTS];
-static uint32_t* g_split[64][QSLOTS];
+// At most EV_LIST_STREAMS streams per device hold lists (created lazily, 16 MB
+// each + 64 MB for split routing); a further stream waits for the device and
+// takes over the oldest entry.
+constexpr int EV_LIST_STREAMS = 8;
+struct EvLists {
+  hipStream_t s;
+  uint32_t* bail;
+  uint32_t* split;
+};
+static EvLists g_lists[64][EV_LIST_STREAMS];
+static int g_nlists[64], g_lnext[64];
 static int g_eocc[3][4][10][64];
 static int g_ff1occ[10][64];
 static int g_ffpocc[4][10][64];
@@ -324,6 +334,27 @@ int pxb_debug_wave_times(unsigned long long* out, unsigned max_waves) {
 #endif
 int pxb_last_hip_error(void) { return g_last_hip; }
 
+// the bailed-id lists of (dev, stream) (callers hold g_mu)
+static int stream_lists(int dev, hipStream_t st, bool need_split, uint32_t** bail, uint32_t** split) {
+  EvLists* e = nullptr;
+  for (int k = 0; k < g_nlists[dev] && !e; ++k)
+    if (g_lists[dev][k].s == st) e = &g_lists[dev][k];
+  if (!e) {
+    if (g_nlists[dev] < EV_LIST_STREAMS) {
+      e = &g_lists[dev][g_nlists[dev]++];
+    } else {                                   // every entry taken: reuse one once the device is idle
+      HIPCHK(hipDeviceSynchronize());
+      e = &g_lists[dev][g_lnext[dev]++ % EV_LIST_STREAMS];
+    }
+    e->s = st;
+  }
+  if (!e->bail) HIPCHK(hipMalloc(&e->bail, (size_t)EV_BAIL_CAP * sizeof(uint32_t)));
+  if (need_split && !e->split) HIPCHK(hipMalloc(&e->split, (size_t)EV_SPLIT_CAP * sizeof(uint32_t)));
+  *bail = e->bail;
+  *split = need_split ? e->split : nullptr;
+  return PXB_OK;
+}
+
 // per-device scratch of pxb_run_device (callers hold g_mu)
 static int ensure_slots(int dev) {
   if (g_slots[dev]) return PXB_OK;
@@ -369,17 +400,17 @@ int pxb_shutdown(void) {
   {
     std::lock_guard<std::mutex> lk(g_mu);
     for (int d = 0; d < 64; ++d) {
-      bool any = g_slots[d] != nullptr;
-      for (int k = 0; k < QSLOTS; ++k) any = any || g_bail[d][k] != nullptr || g_split[d][k] != nullptr;
+      const bool any = g_slots[d] != nullptr || g_nlists[d] > 0;
       if (!any) continue;
       if (hipSetDevice(d) != hipSuccess || hipDeviceSynchronize() != hipSuccess) rc = PXB_E_HIP;
       if (g_slots[d]) (void)hipFree(g_slots[d]);
       g_slots[d] = nullptr;
-      for (int k = 0; k < QSLOTS; ++k) {
-        if (g_bail[d][k]) (void)hipFree(g_bail[d][k]);
-        if (g_split[d][k]) (void)hipFree(g_split[d][k]);
-        g_bail[d][k] = g_split[d][k] = nullptr;
+      for (int k = 0; k < g_nlists[d]; ++k) {
+        if (g_lists[d][k].bail) (void)hipFree(g_lists[d][k].bail);
+        if (g_lists[d][k].split) (void)hipFree(g_lists[d][k].split);
+        g_lists[d][k] = EvLists{};
       }
+      g_nlists[d] = g_lnext[d] = 0;
       g_qseq[d] = 0;
     }
   }
@@ -586,14 +617,8 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
       slot = g_slots[dev] + (size_t)sidx * SLOT_U64;
       kp.part = slot;
       kp.queue = reinterpret_cast<uint32_t*>(slot + 2 * ROWS_U64);
-      if (use_ev || use_ff1 || use_ffp) {
-        if (!g_bail[dev][sidx]) HIPCHK(hipMalloc(&g_bail[dev][sidx], (size_t)EV_BAIL_CAP * sizeof(uint32_t)));
-        bail = g_bail[dev][sidx];
-      }
-      if (split) {
-        if (!g_split[dev][sidx]) HIPCHK(hipMalloc(&g_split[dev][sidx], (size_t)EV_SPLIT_CAP * sizeof(uint32_t)));
-        slist = g_split[dev][sidx];
-      }
+      if (use_ev || use_ff1 || use_ffp)
+        if (int rc2 = stream_lists(dev, st, split, &bail, &slist)) return rc2;
     }
     // a launch that fails after an earlier one of this chunk has queued leaves
     // the slot half used: zero it behind the queued work before reporting

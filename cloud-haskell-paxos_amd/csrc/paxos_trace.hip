@@ -11,10 +11,12 @@
 namespace pxb {
 namespace ev {
 
-template <int PM, int N, int POOL, int W, class Mem>
-__device__ void trace_record(const EvLane<PM, N, POOL, W, false, Mem, false>& L, uint32_t step, pxb_trace_step* r) {
+template <int PM, int N, int POOL, int W, class Mem, bool EARLY>
+__device__ void trace_record(const EvLane<PM, N, POOL, W, false, Mem, EARLY>& L, uint32_t step, pxb_trace_step* r) {
   r->step = step;
-  r->in_flight = L.in_flight;
+  // (production variant: copies of a broadcast still to send are not on the
+  // links yet, so the count is not the oracle's end-of-step one)
+  r->in_flight = (EARLY && L.pq_len != 0u) ? PXB_TRACE_IN_FLIGHT_UNKNOWN : L.in_flight;
   r->n_acceptors = N;
   r->n_proposers = L.P;
   for (int a = 0; a < PXB_MAX_ACCEPTORS; ++a) {
@@ -44,15 +46,19 @@ __device__ void trace_record(const EvLane<PM, N, POOL, W, false, Mem, false>& L,
 }
 
 // one wave, lane 0 runs the instance; status[0] = records written,
-// status[1] = 1 bailed / 2 out of records
-template <int PM, int N, int W>
+// status[1] = 1 bailed / 2 out of records.  EARLY = false (the default trace):
+// every step drains its copies, so each record is the oracle's end-of-step
+// state exactly; EARLY = true (PXB_CFG_TRACE_PRODUCTION): the carry-over
+// variant the batch kernels run (paxos_ev.h, end_op), recorded on entering the
+// next step.
+template <int PM, int N, int W, bool EARLY>
 __global__ __launch_bounds__(64) void paxos_trace_kernel(EvParams p, uint32_t gid, pxb_trace_step* out, uint32_t max,
                                                          uint32_t* status, uint4* res) {
   constexpr int POOL = EvPool<PM, N, false>::value;
   using S = Shape<PM, N, POOL, W, false>;
   __shared__ uint32_t lds[S::WORDS * 64];
   if (threadIdx.x != 0) return;
-  EvLane<PM, N, POOL, W, false, LdsMem, false> L;   // every step drains its copies: see EARLY
+  EvLane<PM, N, POOL, W, false, LdsMem, EARLY> L;
   L.m = LdsMem{lds, 0u};
   L.set_keys(p);
   L.init(p, gid);
@@ -66,12 +72,16 @@ __global__ __launch_bounds__(64) void paxos_trace_kernel(EvParams p, uint32_t gi
       break;
     }
     if (done || L.s != s0) {
-      if (n >= max) {
+      const uint32_t step = (uint32_t)(done ? L.s : s0);
+      // (production variant: an instance whose carried step held only lost
+      // copies ends at the step before it, already recorded: rewrite that record)
+      const bool again = EARLY && done && n > 0 && out[n - 1].step == step;
+      if (!again && n >= max) {
         status[1] = 2u;
         break;
       }
-      trace_record(L, (uint32_t)(done ? L.s : s0), out + n);
-      ++n;
+      trace_record(L, step, out + (again ? n - 1 : n));
+      n += again ? 0u : 1u;
     }
     if (done) {
       *res = make_uint4(o.res[0], o.res[1], o.res[2], o.res[3]);
@@ -83,29 +93,30 @@ __global__ __launch_bounds__(64) void paxos_trace_kernel(EvParams p, uint32_t gi
 
 typedef void (*trace_ptr)(EvParams, uint32_t, pxb_trace_step*, uint32_t, uint32_t*, uint4*);
 
-template <int PM, int W>
+template <int PM, int W, bool E>
 static trace_ptr pick_n(uint32_t n) {
   switch (n) {
-    case 2: return paxos_trace_kernel<PM, 2, W>;
-    case 3: return paxos_trace_kernel<PM, 3, W>;
-    case 4: return paxos_trace_kernel<PM, 4, W>;
-    case 5: return paxos_trace_kernel<PM, 5, W>;
-    case 6: return paxos_trace_kernel<PM, 6, W>;
-    case 7: return paxos_trace_kernel<PM, 7, W>;
-    case 8: return paxos_trace_kernel<PM, 8, W>;
-    case 9: return paxos_trace_kernel<PM, 9, W>;
+    case 2: return paxos_trace_kernel<PM, 2, W, E>;
+    case 3: return paxos_trace_kernel<PM, 3, W, E>;
+    case 4: return paxos_trace_kernel<PM, 4, W, E>;
+    case 5: return paxos_trace_kernel<PM, 5, W, E>;
+    case 6: return paxos_trace_kernel<PM, 6, W, E>;
+    case 7: return paxos_trace_kernel<PM, 7, W, E>;
+    case 8: return paxos_trace_kernel<PM, 8, W, E>;
+    case 9: return paxos_trace_kernel<PM, 9, W, E>;
   }
   return nullptr;
 }
 
+template <bool E>
 static trace_ptr pick(uint32_t pm, uint32_t n, int w) {
   switch (pm * 100 + (uint32_t)w) {
-    case 108: return pick_n<1, 8>(n);
-    case 116: return pick_n<1, 16>(n);
-    case 208: return pick_n<2, 8>(n);
-    case 216: return pick_n<2, 16>(n);
-    case 308: return pick_n<3, 8>(n);
-    case 316: return pick_n<3, 16>(n);
+    case 108: return pick_n<1, 8, E>(n);
+    case 116: return pick_n<1, 16, E>(n);
+    case 208: return pick_n<2, 8, E>(n);
+    case 216: return pick_n<2, 16, E>(n);
+    case 308: return pick_n<3, 8, E>(n);
+    case 316: return pick_n<3, 16, E>(n);
   }
   return nullptr;
 }
@@ -123,7 +134,9 @@ extern "C" int pxb_trace_instance(const pxb_config* cfg, uint64_t instance, pxb_
     return PXB_E_INVAL;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return PXB_E_NODEV;
-  const trace_ptr fn = pick(cfg->n_proposers, cfg->n_acceptors, wheel_for(cfg->delay_max));
+  const bool prod = (cfg->flags & PXB_CFG_TRACE_PRODUCTION) != 0u;
+  const trace_ptr fn = prod ? pick<true>(cfg->n_proposers, cfg->n_acceptors, wheel_for(cfg->delay_max))
+                            : pick<false>(cfg->n_proposers, cfg->n_acceptors, wheel_for(cfg->delay_max));
   if (!fn) return PXB_E_INVAL;
   EvParams p = make_params(cfg);
   p.first_instance = instance;

@@ -27,6 +27,8 @@ PXB_OK, PXB_E_INVAL, PXB_E_HIP, PXB_E_OOM, PXB_E_NODEV, PXB_E_RCCL = 0, -1, -2, 
 MAX_PROPOSERS, MIN_ACCEPTORS, MAX_ACCEPTORS = 3, 2, 9
 MAX_DELAY, MAX_STEP_CAP, QUEUE_DEPTH, LOG_TRACK, MAX_TICKS = 15, 8192, 8, 32, 4096
 CFG_RANDOMIZE = 1
+CFG_TRACE_PRODUCTION = 2         # pxb_trace_instance: the batch kernels' carry-over variant
+TRACE_IN_FLIGHT_UNKNOWN = 0xFFFFFFFF
 
 F_UNDECIDED, F_STUCK, F_PANIC, F_LOG_DIVERGENCE = 1, 2, 4, 8
 F_STEP_CAP, F_QUEUE_OVERFLOW, F_TICKET_OVERFLOW, F_LOG_TRUNC = 16, 32, 64, 128
@@ -264,6 +266,18 @@ def _check_buf(name, t, words, itemsize):
         raise ValueError("%s: %d elements, %d needed" % (name, t.numel(), words))
 
 
+def _check_bytes(name, t, nbytes):
+    """A device byte buffer: contiguous GPU uint8 tensor of at least nbytes
+    (its element count is the byte bound handed to the C ABI)."""
+    import torch
+    if not getattr(t, "is_cuda", False):
+        raise ValueError("%s: a CUDA (HIP) tensor is required" % name)
+    if t.dtype != torch.uint8 or not t.is_contiguous():
+        raise ValueError("%s: contiguous uint8 tensor required" % name)
+    if t.numel() < nbytes:
+        raise ValueError("%s: %d bytes, %d needed" % (name, t.numel(), nbytes))
+
+
 def run_device(cfg: Config, first_instance: int, n_instances: int, d_results=None,
                d_digests=None, d_acceptors=None, d_totals=None, stream=None):
     """Device-buffer, asynchronous batch run (pxb_run_device) on torch tensors
@@ -332,9 +346,11 @@ def wire_encode_device(d_msgs, wire_type, d_offsets, d_bytes, stream=None):
     """Fused size + encode on device tensors (pxb_wire_encode_all): d_msgs
     int32 (n, 4), d_offsets int64 (n + 1), d_bytes uint8 (n * WIRE_MAX_BYTES),
     asynchronous on `stream` (a raw hipStream_t handle, default stream if None)."""
-    lib = load()
     n = d_msgs.shape[0]
-    assert d_offsets.numel() >= n + 1 and d_bytes.numel() >= max(1, n * WIRE_MAX_BYTES)
+    _check_buf("d_msgs", d_msgs, 4 * n, 4)
+    _check_bytes("d_bytes", d_bytes, max(1, n * WIRE_MAX_BYTES))
+    _check_buf("d_offsets", d_offsets, n + 1, 8)
+    lib = load()
     check(lib.pxb_wire_encode_all(C.c_void_p(d_msgs.data_ptr()), n, wire_type, C.c_void_p(d_offsets.data_ptr()),
                                   C.c_void_p(d_bytes.data_ptr()), C.c_void_p(stream or 0)))
 
@@ -343,8 +359,11 @@ def wire_decode_device(d_bytes, d_offsets, n, wire_type, d_msgs, d_status=None, 
     """pxb_wire_decode on device tensors: d_bytes uint8 (its whole length is the
     buffer bound), d_offsets int64 (n + 1), d_msgs int32 (n, 4), d_status int32
     (n,) or None; asynchronous on `stream` (raw hipStream_t, default if None)."""
+    _check_bytes("d_bytes", d_bytes, 1)
+    _check_buf("d_offsets", d_offsets, n + 1, 8)
+    _check_buf("d_msgs", d_msgs, 4 * n, 4)
+    _check_buf("d_status", d_status, n, 4)
     lib = load()
-    assert d_offsets.numel() >= n + 1 and d_msgs.shape[0] >= n
     check(lib.pxb_wire_decode(C.c_void_p(d_bytes.data_ptr()), d_bytes.numel(), C.c_void_p(d_offsets.data_ptr()), n,
                               wire_type, C.c_void_p(d_msgs.data_ptr()),
                               C.c_void_p(d_status.data_ptr() if d_status is not None else 0), C.c_void_p(stream or 0)))
@@ -353,17 +372,20 @@ def wire_decode_device(d_bytes, d_offsets, n, wire_type, d_msgs, d_status=None, 
 TRACE_WORDS = 4 + 9 * 4 + 9 + 3 * 8      # pxb_trace_step, uint32 words
 
 
-def trace_instance(cfg: Config, instance: int, max_records: int = 8192):
+def trace_instance(cfg: Config, instance: int, max_records: int = 8192, production: bool = False):
     """pxb_trace_instance: the state at the end of every visited step of one
     instance, as a list of dicts (step, in_flight, acc (N, 4), digest (N,),
     prop (P, 8): ticket, cmd, acks, state, mr_t, mr_v, r2_v, pending), and its
-    pxb_result."""
+    pxb_result.  production=True traces the batch kernels' carry-over variant
+    (PXB_CFG_TRACE_PRODUCTION; in_flight may be TRACE_IN_FLIGHT_UNKNOWN)."""
     import numpy as np
     lib = load()
     buf = np.zeros((max_records, TRACE_WORDS), dtype=np.uint32)
     nrec = C.c_uint32(0)
     res = np.zeros(4, dtype=np.uint32)
     c = cfg.to_c(instance, 1)
+    if production:
+        c.flags |= CFG_TRACE_PRODUCTION
     check(lib.pxb_trace_instance(C.byref(c), instance, _ptr(buf), max_records, C.byref(nrec), _ptr(res)))
     out = []
     for r in buf[:nrec.value]:

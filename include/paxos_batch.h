@@ -51,6 +51,12 @@ extern "C" {
 #define PXB_CFG_RANDOMIZE 1u     /* config-5 fuzz: per-instance P, loss, delay,
                                     crash drawn from Philox (n_proposers,
                                     loss_ppm, delay_max, crash_ppm are maxima) */
+#define PXB_CFG_TRACE_PRODUCTION 2u  /* pxb_trace_instance only (batch runs ignore
+                                    it): trace the carry-over variant the batch
+                                    kernels run instead of the draining one    */
+#define PXB_TRACE_IN_FLIGHT_UNKNOWN 0xFFFFFFFFu  /* trace record: copies of a
+                                    broadcast not yet on the links (production
+                                    variant), so no end-of-step count          */
 
 /* Everything that defines a batch.  Mirrors the hard-coded constants of the
  * reference (N = 2 acceptors Main.hs:41, P = 2 proposers Main.hs:45, majority
@@ -165,10 +171,14 @@ int pxb_run_multi(const pxb_config* cfg, int n_devices, pxb_result* out, uint32_
 
 /* ---- context ------------------------------------------------------------------
  * The library keeps per-device scratch (64 launch slots of partial totals and
- * queue words, the per-lane kernel's bailed-id lists, the wire codec's scan
- * buffer) and the RCCL communicators of pxb_run_multi, created lazily on
- * first use.  pxb_init(n) creates the scratch of devices 0..n-1 (n <= 0: all
- * visible) up front; pxb_shutdown() waits for those devices, frees everything
+ * queue words, 2 MB per device; the wire codec's scan buffer) and the RCCL
+ * communicators of pxb_run_multi, created lazily on first use.  The per-lane
+ * kernels' bailed-id lists are kept per (device, stream) of pxb_run_device,
+ * allocated on that stream's first faulty or per-lane launch: 16 MB each, plus
+ * 64 MB for the split routing of fuzzed three-proposer batches, for at most 8
+ * streams per device (a ninth stream waits for the device and takes over an
+ * existing entry).  pxb_init(n) creates the launch slots of devices 0..n-1
+ * (n <= 0: all visible) up front; pxb_shutdown() waits for those devices, frees everything
  * and destroys the communicators; the next call starts afresh.  Both are
  * optional.  Do not call pxb_shutdown while other threads have calls in
  * flight.  (A CPU pxb_run_cpu is NOT part of this library: the CPU
@@ -185,7 +195,16 @@ int pxb_shutdown(void);
  * no Tick change nothing and are skipped (their state is the previous
  * record's).  Host buffers; out holds max_records records; *n_records is the
  * count written (the last one is the final step); result (nullable) is the
- * instance's pxb_result, as pxb_run gives it.  PXB_E_INVAL for log mode, for
+ * instance's pxb_result, as pxb_run gives it.  By default the trace runs the
+ * variant of the state machine in which every step sends all of its copies
+ * before the next begins, so every record is the schedule's end-of-step state.
+ * The batch kernels run a variant that may carry the copies of a step's last
+ * broadcast into the next step; with PXB_CFG_TRACE_PRODUCTION in cfg->flags the
+ * trace runs that variant instead: records are taken on entering the next step
+ * (acceptor and proposer states are the end-of-step ones; in_flight is
+ * PXB_TRACE_IN_FLIGHT_UNKNOWN while copies are still to send, and a carried
+ * step may be recorded although nothing else falls due in it).
+ * PXB_E_INVAL for log mode, for
  * step_cap > 4095, or if the instance outgrows the state machine's link
  * capacities (its FIFOs hold 4 messages; the batch kernels then hand it to
  * the general kernel) or max_records.                                        */

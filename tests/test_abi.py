@@ -139,3 +139,28 @@ def test_run_device_checks_buffers_before_the_abi():
         pxb.run_device(cfg, 0, n, d_results=Fake(4 * n, 4, False), d_totals=Fake(16, 8))
     with pytest.raises(ValueError, match="needed"):
         pxb.run_device(cfg, 0, n, d_totals=Fake(15, 8))
+
+
+def test_wire_device_entry_points_check_their_buffers():
+    """The device wire calls take raw pointers: host tensors, wrong dtypes and
+    short buffers are refused before anything reaches the C ABI."""
+    import torch
+    n = 4
+    msgs = torch.zeros((n, 4), dtype=torch.int32)
+    offs = torch.zeros(n + 1, dtype=torch.int64)
+    byts = torch.zeros(n * pxb.WIRE_MAX_BYTES, dtype=torch.uint8)
+    with pytest.raises(ValueError, match="CUDA"):
+        pxb.wire_encode_device(msgs, pxb.WIRE_RESPONSE, offs, byts)
+    with pytest.raises(ValueError, match="CUDA"):
+        pxb.wire_decode_device(byts, offs, n, pxb.WIRE_RESPONSE, msgs)
+    class _PosingAsDevice:                # a device-looking int32 buffer reaches the dtype check
+        is_cuda = True
+        dtype = torch.int32
+
+        def is_contiguous(self):
+            return True
+
+        def numel(self):
+            return 64
+    with pytest.raises(ValueError, match="uint8"):
+        pxb._check_bytes("d_bytes", _PosingAsDevice(), 1)

@@ -32,6 +32,13 @@ def test_bench_launcher_ranks(gpus):
     assert j["n_gpus"] == gpus and j["rccl_world"] == gpus
     assert j["counters"]["instances"] == 500 * 3 * gpus     # all-reduced over the ranks
     assert j["steps"] == 3 and j["ms_per_step"] > 0
+    # the north-star line: one fixed batch (the dry-run stand-in for 2^26)
+    # split over the ranks, strong scaling, totals all-reduced
+    ns = j["north_star"]
+    assert ns["n_gpus"] == gpus and ns["rccl_world"] == gpus and ns["scaling"] == "strong"
+    assert ns["instances_per_gpu_per_step"] * gpus == ns["instances_per_step"] == 1 << 12
+    assert ns["counters"]["instances"] == 1 << 12
+    assert ns["instances_per_s"] > 0
 
 
 def test_bench_rejects_world_mismatch():
@@ -39,3 +46,14 @@ def test_bench_rejects_world_mismatch():
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run", "--gpus", "2"],
                          capture_output=True, text=True, timeout=120, env={**os.environ, **env}, cwd=ROOT)
     assert out.returncode != 0 and "WORLD_SIZE" in out.stderr
+
+
+def test_step_instances_sized_from_world():
+    """Configs 4 and 5 are one batch over the node (64M over 8 GPUs, 256M):
+    each rank's share is that batch / world; config 2 is a fixed batch per GPU."""
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.step_instances(4, 0, 1) == 1 << 26 and bench.step_instances(4, 0, 8) == 1 << 23
+    assert bench.step_instances(5, 0, 8) == 1 << 25 and bench.step_instances(5, 0, 2) == 1 << 27
+    assert bench.step_instances(2, 0, 1) == bench.step_instances(2, 0, 8) == 1 << 28
+    assert bench.scaling_of(4) == "strong" and bench.scaling_of(2) == "weak"

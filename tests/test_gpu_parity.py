@@ -590,3 +590,41 @@ def test_trace_matches_oracle_steps(gpu_lib, c, inst):
                 {k: prev[k] for k in ("acc", "digest", "prop", "in_flight")}, r["step"]
     assert cur is None and g[-1]["step"] == want[-1]["step"] and by_step
     assert list(gres) == [res.decided_val, res.decided_ticket, res.rounds, res.packed_flags()]
+
+
+@pytest.mark.parametrize("c,inst", [(3, 0), (3, 17), (4, 5), (4, 123456), (5, 9), (5, 1000), (4, 77), (3, 4242)])
+def test_trace_production_variant_matches_oracle_steps(gpu_lib, c, inst):
+    """The carry-over variant the batch kernels run (a step may end with the
+    copies of its last broadcast still to send): at every step it records, the
+    acceptor records, log digests and proposer states equal the oracle's state
+    at the end of that step (or of the last step the oracle visited before it:
+    a carried step may hold nothing else); the oracle steps it skips change
+    nothing; in_flight equals the oracle's whenever no copy is pending."""
+    cfg = pxb.CONFIGS[c]
+    try:
+        g, gres = pxb.trace_instance(cfg, inst, production=True)
+    except pxb.PaxosError:
+        pytest.skip("instance beyond the trace kernel's link capacities")
+    want, res = _oracle_trace(cfg, inst)
+    steps = [r["step"] for r in want]
+    gsteps = [int(x["step"]) for x in g]
+    assert gsteps == sorted(set(gsteps))
+    keys = ("acc", "digest", "prop", "in_flight")
+    for k, r in enumerate(want):                       # skipped steps change nothing
+        if r["step"] not in gsteps:
+            assert k > 0 and {q: r[q] for q in keys} == {q: want[k - 1][q] for q in keys}, r["step"]
+    import bisect
+    carried = 0
+    for x in g:
+        r = _as_rec(x)
+        k = bisect.bisect_right(steps, r["step"]) - 1
+        assert k >= 0, r["step"]
+        w = want[k]
+        for key in ("acc", "digest", "prop"):
+            assert r[key] == w[key], "step %d %s: oracle %s gpu %s" % (r["step"], key, w[key], r[key])
+        if r["in_flight"] != pxb.TRACE_IN_FLIGHT_UNKNOWN:
+            assert r["in_flight"] == w["in_flight"], r["step"]
+        else:
+            carried += 1
+    assert gsteps[-1] == steps[-1]
+    assert list(gres) == [res.decided_val, res.decided_ticket, res.rounds, res.packed_flags()]

@@ -22,13 +22,21 @@ from collections import defaultdict
 CUS = 256
 PEAK_CLOCK_HZ = 2.4e9
 VALU_PER_CU_CYCLE = 2.0
-KERNEL_TAGS = ("paxos_ev_kernel", "paxos_ff1_kernel", "paxos_batch_kernel", "finalize_kernel")
+KERNEL_TAGS = ("paxos_ev_kernel", "paxos_ff1_kernel", "paxos_ffp_kernel", "paxos_evl_kernel",
+               "paxos_batch_kernel", "finalize_kernel")
+# kernels a profiled bench command may also run that are not part of a step
+# (torch's own fills and copies, the wire codec's passes)
+IGNORED = ("elementwise", "fill", "copy", "memset", "Memset", "Memcpy", "tile_sum", "encode_kernel",
+           "decode_kernel", "DeviceScan", "hook_kernel")
 
 
 def _tag(name):
     for t in KERNEL_TAGS:
         if t in name:
             return t
+    if name and not any(i in name for i in IGNORED):
+        # an untagged kernel would silently drop out of the per-instance sums
+        raise SystemExit("roofline.py: profiled kernel %r matches no KERNEL_TAGS entry" % name)
     return None
 
 
