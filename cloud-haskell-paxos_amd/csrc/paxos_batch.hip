@@ -169,18 +169,21 @@ static ffp_kernel_ptr ffp_pick(uint32_t p, uint32_t n) {
   return p == 1 ? ffp_pick_n<1>(n) : p == 2 ? ffp_pick_n<2>(n) : p == 3 ? ffp_pick_n<3>(n) : nullptr;
 }
 
-// layout index: 0 = 8-step wheel, 1 = 16-step wheel, 2 = compact links (8-step wheel)
+// layout index: 0 = 8-step wheel, 1 = 16-step wheel, 2 / 3 = compact links (8- / 4-step wheel)
 static ev_kernel_ptr ev_pick(uint32_t pm, uint32_t n, int layout) {
   switch (pm * 10 + (uint32_t)layout) {
     case 10: return ev_pick_n<1, 8, false>(n);
     case 11: return ev_pick_n<1, 16, false>(n);
     case 12: return ev_pick_n<1, 8, true>(n);
+    case 13: return ev_pick_n<1, 4, true>(n);
     case 20: return ev_pick_n<2, 8, false>(n);
     case 21: return ev_pick_n<2, 16, false>(n);
     case 22: return ev_pick_n<2, 8, true>(n);
+    case 23: return ev_pick_n<2, 4, true>(n);
     case 30: return ev_pick_n<3, 8, false>(n);
     case 31: return ev_pick_n<3, 16, false>(n);
     case 32: return ev_pick_n<3, 8, true>(n);
+    case 33: return ev_pick_n<3, 4, true>(n);
   }
   return nullptr;
 }
@@ -273,7 +276,7 @@ struct EvLists {
 };
 static EvLists g_lists[64][EV_LIST_STREAMS];
 static int g_nlists[64], g_lnext[64];
-static int g_eocc[3][4][10][64];
+static int g_eocc[4][4][10][64];
 static int g_ff1occ[10][64];
 static int g_ffpocc[4][10][64];
 

@@ -130,6 +130,16 @@ __host__ __device__ inline uint64_t ev_threshold(uint32_t ppm) {
   return ((((uint64_t)ppm) << 32) + 999999ull) / 1000000ull;
 }
 
+// true in every lane when the predicate holds in any lane of the wave (host: the
+// lane's own value): guards code that only a few lanes of a wave ever need
+__host__ __device__ __forceinline__ bool any_lane(bool p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_ballot_w64(p) != 0ull;
+#else
+  return p;
+#endif
+}
+
 __host__ __device__ __forceinline__ uint32_t ctz32(uint32_t x) { return x ? (uint32_t)__builtin_ctz(x) : 32u; }
 __host__ __device__ __forceinline__ uint32_t popc32(uint32_t x) { return (uint32_t)__builtin_popcount(x); }
 
@@ -217,7 +227,12 @@ struct EvLane {
 #endif
   }
   __host__ __device__ static __forceinline__ uint32_t bfi(uint32_t mk, uint32_t x, uint32_t y) {
-#if defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__) && defined(PXB_EV_BITOP3_BFI)
+    // (v_bitop3_b32 with the bitwise-select table, 0xCA, as a builtin: no
+    // s_nop before each dependent select, but LLVM then adds copies around it;
+    // MI355X A/B: config 4 -7 %, config 3 -1 %: not used)
+    return __builtin_amdgcn_bitop3_b32(mk, x, y, 0xCA);
+#elif defined(__HIP_DEVICE_COMPILE__)
     uint32_t r;
     __asm__("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(mk), "v"(x), "v"(y));
     return r;
@@ -259,6 +274,16 @@ struct EvLane {
   __host__ __device__ uint32_t p_r2_v(int p) const { return (pw1[p] >> 2) & 3u; }
   __host__ __device__ uint32_t p_cmd(int p) const { return (pw1[p] >> 4) & 3u; }
 
+  // broadcast ring slot `slot` of proposer q: halfword `half` of word `word`
+  // (two proposers: one word per slot, the proposer picks the half)
+  __host__ __device__ static __forceinline__ uint32_t bring_word(uint32_t q, uint32_t slot) {
+    if (PM == 2) return slot;
+    return q * (S::BR / 2u) + (slot >> 1);
+  }
+  __host__ __device__ static __forceinline__ uint32_t bring_half(uint32_t q, uint32_t slot) {
+    if (PM == 2) return q;
+    return slot & 1u;
+  }
   __host__ __device__ __forceinline__ uint32_t rsp_ld(uint32_t Lr) const { return m.ld(S::RSP + Lr); }
   __host__ __device__ __forceinline__ void rsp_st(uint32_t Lr, uint32_t v) const { m.st(S::RSP + Lr, v); }
 
@@ -291,7 +316,9 @@ struct EvLane {
     occ &= ~(1u << slot);
     acc_mask = wq;
     // Ticks only up to the last skew
-    in_mask = wi | ((t <= last_tick) ? ticks_at(t) : 0u);
+    uint32_t tk = 0u;
+    if (any_lane(t <= last_tick)) tk = (t <= last_tick) ? ticks_at(t) : 0u;   // (first steps only)
+    in_mask = wi | tk;
 #pragma unroll
     for (int p = 0; p < PM; ++p) {
       const uint32_t grp = ((1u << (N + 1)) - 1u) << (p * (N + 1));
@@ -399,8 +426,8 @@ struct EvLane {
     // (non-short-circuit: || here became two exec-mask branches)
     bailed = bailed | (p0 & (((rc >> (4u * slot0)) & 15u) != 0u)) | (p1 & (((rc >> (4u * slot1)) & 15u) != 0u));
     if (p0) {                                        // (p1 only with p0)
-      m.st16(S::BRING, q * S::BR + slot0, x0 | (z0 << 12) | (kind0 << 14));
-      if (p1) m.st16(S::BRING, q * S::BR + slot1, x1 | (ASK << 14));
+      m.st16h(S::BRING + bring_word(q, slot0), bring_half(q, slot0), x0 | (z0 << 12) | (kind0 << 14));
+      if (p1) m.st16h(S::BRING + bring_word(q, slot1), bring_half(q, slot1), x1 | (ASK << 14));
     }
     pq |= (p0 ? ((q << 3) | slot0) << (5u * pq_len) : 0u) | (p1 ? ((q << 3) | slot1) << (5u * pq_len + 5u) : 0u);
     pq_len += (p0 ? 1u : 0u) + (p1 ? 1u : 0u);
@@ -575,7 +602,7 @@ struct EvLane {
     const bool keep = (len > 1u) & (((wq >> 10) & 15u) == s4);   // the next entry due now too
     acc_mask = (acc & !keep) ? (acc_mask & ~(1u << L)) : acc_mask;
     in_flight -= acc ? 1u : 0u;
-    const uint32_t w16 = m.ld16(S::BRING, p * S::BR + bslot);
+    const uint32_t w16 = m.ld16h(S::BRING + bring_word(p, bslot), bring_half(p, bslot));
     put(refc, p, get(refc, p) - (acc ? 1u << (4u * bslot) : 0u));
     const uint32_t kind = w16 >> 14, x = w16 & 0xFFFu, z = (w16 >> 12) & 3u;
     const uint32_t A = get(accw, a);
@@ -723,6 +750,7 @@ struct EvLane {
       const uint32_t s1 = (uint32_t)s + 1u;
       const uint32_t rot = ((occ >> (s1 & WM)) | (occ << ((W - (s1 & WM)) & WM))) & ((1u << W) - 1u);
       uint32_t nx = ((occ != 0u) & (pq_len == 0u)) ? s1 + ctz32(rot) : (pq_len ? s1 : 0xFFFFu);
+      if (any_lane(s < last_tick))                    // (a later Tick: first steps only)
 #pragma unroll
       for (int q = 0; q < PM; ++q) nx = ((skew[q] > (uint32_t)s) & (skew[q] < nx)) ? skew[q] : nx;
       const bool capped = !quiet & (nx >= kp.step_cap);
@@ -803,7 +831,9 @@ __host__ inline EvParams make_params(const pxb_config* c) {
 // the timing wheel must outlast the longest delay: sends at step s (or s - 1
 // for a carried-over copy) fall due in [s, s + delay_max] (a link's FIFO tail
 // is at most its last send step + delay_max), the slot of s is emptied on
-// entering s, so 8 slots serve delays up to 8
+// entering s and a copy due at s goes straight to the step's due links, so
+// the wheel holds dues in [s + 1, s + delay_max]: 8 slots serve delays up to 8
+// (4 slots up to 4)
 __host__ inline int wheel_for(uint32_t delay_max) { return delay_max <= 8 ? 8 : 16; }
 
 // Kernel layout of a launch: 0 = 8-step wheel, 1 = 16-step wheel, 2 = compact
@@ -816,12 +846,16 @@ __host__ inline int wheel_for(uint32_t delay_max) { return delay_max <= 8 ? 8 : 
 // steps), so long runs keep the separate 16-bit one; three duelling proposers
 // over 9 acceptors overflow the 3-entry FIFOs too often (25 % of instances at
 // 10 % loss), so the compact layout is kept to topologies of <= 16 links.
+// Layout 3 is the compact layout with a 4-step wheel (delays up to 4: BASELINE
+// configs 3 and 4), 4 words per lane fewer.
 __host__ inline int layout_for(const pxb_config* c) {
   if (!(c->flags & PXB_CFG_RANDOMIZE) && c->delay_max <= 4 && c->step_cap <= 512 &&
       c->n_proposers * c->n_acceptors <= 16)
-    return 2;
+    return 3;
   return wheel_for(c->delay_max) == 8 ? 0 : 1;
 }
+__host__ inline int layout_wheel(int layout) { return layout == 1 ? 16 : layout == 3 ? 4 : 8; }
+__host__ inline bool layout_compact(int layout) { return layout >= 2; }
 
 }  // namespace ev
 }  // namespace pxb

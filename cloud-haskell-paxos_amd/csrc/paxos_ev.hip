@@ -1,7 +1,7 @@
 // paxos_ev.hip — explicit instantiations of the per-lane kernel
 // (paxos_ev_kernel.h) for one proposer count (-DPXB_EV_P=1|2|3): 8 acceptor
 // counts x {8, 16}-step timing wheels (plus the compact-link
-// layout with the 8-step wheel).  Split by P so the units build in
+// layout with the 8- and 4-step wheels).  Split by P so the units build in
 // parallel.
 #include "paxos_ev_kernel.h"
 
@@ -17,5 +17,6 @@ namespace ev {
 PXB_EV_FOR_N(8, false)
 PXB_EV_FOR_N(16, false)
 PXB_EV_FOR_N(8, true)
+PXB_EV_FOR_N(4, true)
 }  // namespace ev
 }  // namespace pxb

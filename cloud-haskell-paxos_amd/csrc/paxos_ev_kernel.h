@@ -27,6 +27,13 @@ struct LdsMem {
   __host__ __device__ void st16(uint32_t base, uint32_t i, uint32_t v) const {
     reinterpret_cast<uint16_t*>(w)[((base + (i >> 1)) * 64u + lane) * 2u + (i & 1u)] = (uint16_t)v;
   }
+  // halfword `half` (0, 1) of word i
+  __host__ __device__ uint32_t ld16h(uint32_t i, uint32_t half) const {
+    return reinterpret_cast<const uint16_t*>(w)[(i * 64u + lane) * 2u + half];
+  }
+  __host__ __device__ void st16h(uint32_t i, uint32_t half, uint32_t v) const {
+    reinterpret_cast<uint16_t*>(w)[(i * 64u + lane) * 2u + half] = (uint16_t)v;
+  }
   // OR into a word (ds_or_b32: no read-back on the critical path)
   __device__ void orw(uint32_t i, uint32_t v) const { atomicOr(&w[i * 64u + lane], v); }
 };
@@ -56,9 +63,12 @@ struct EvKParams {
 
 // response-pool words per lane of a shape (the compact layout is picked for
 // schedules with short delays, whose responses in flight stay fewer)
+#ifndef PXB_EV_CMP_POOL
+#define PXB_EV_CMP_POOL 24
+#endif
 template <int PM, int N, bool CMP>
 struct EvPool {
-  static constexpr int value = (PM * N <= 16) ? (CMP ? 24 : 32) : CMP ? 48 : (PM * N <= 18) ? 32 : 64;
+  static constexpr int value = (PM * N <= 16) ? (CMP ? PXB_EV_CMP_POOL : 32) : CMP ? 48 : (PM * N <= 18) ? 32 : 64;
 };
 
 // Run totals: each lane sums its finished instances in registers; the wave

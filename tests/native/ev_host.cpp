@@ -22,6 +22,8 @@ struct HostMem {
   void st(uint32_t i, uint32_t v) const { w[i] = v; }
   uint32_t ld16(uint32_t base, uint32_t i) const { return reinterpret_cast<const uint16_t*>(w + base)[i]; }
   void st16(uint32_t base, uint32_t i, uint32_t v) const { reinterpret_cast<uint16_t*>(w + base)[i] = (uint16_t)v; }
+  uint32_t ld16h(uint32_t i, uint32_t half) const { return reinterpret_cast<const uint16_t*>(w + i)[half]; }
+  void st16h(uint32_t i, uint32_t half, uint32_t v) const { reinterpret_cast<uint16_t*>(w + i)[half] = (uint16_t)v; }
   void orw(uint32_t i, uint32_t v) const { w[i] |= v; }
 };
 
@@ -120,6 +122,7 @@ extern "C" int ev_host_run(const pxb_config* cfg, pxb_result* out, uint32_t* dig
   const char* lv = getenv("EV_LAYOUT");                 // tests: force a layout
   const int layout = lv ? atoi(lv) : layout_for(cfg);
   if (layout == 2 && cfg->delay_max > 8) return -1;
+  if (layout == 3 && cfg->delay_max > 4) return -1;
   if (layout == 0 && cfg->delay_max > 8) return -1;
   // tests: the shape's proposer capacity; below n_proposers (fuzzed batches
   // only) it is the split routing of pxb_run_device, whose instances with more
@@ -134,6 +137,7 @@ extern "C" int ev_host_run(const pxb_config* cfg, pxb_result* out, uint32_t* dig
     case 0: return run_w<8, false>(cfg, pm, out, dig, acc, totals, bail_ids, n_bail, micro_steps);
     case 1: return run_w<16, false>(cfg, pm, out, dig, acc, totals, bail_ids, n_bail, micro_steps);
     case 2: return run_w<8, true>(cfg, pm, out, dig, acc, totals, bail_ids, n_bail, micro_steps);
+    case 3: return run_w<4, true>(cfg, pm, out, dig, acc, totals, bail_ids, n_bail, micro_steps);
   }
   return -1;
 }

@@ -19,7 +19,10 @@ import pxb
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "native", "ev_host.cpp")
-OUT = os.path.join(HERE, "native", "_build", "libev_host.so")
+# PXB_EV_HOST_DEFS="-DX -DY": build the state machine with extra defines (kernel
+# variants under evaluation) into a library of its own
+DEFS = os.environ.get("PXB_EV_HOST_DEFS", "").split()
+OUT = os.path.join(HERE, "native", "_build", "libev_host%s.so" % ("".join(d.replace("-D", "_") for d in DEFS)))
 DEPS = [SRC] + [os.path.join(HERE, "..", "cloud-haskell-paxos_amd", "csrc", f)
                 for f in ("paxos_ev.h", "paxos_ev_kernel.h", "paxos_device.h")] + [os.path.join(HERE, "..", "include", "paxos_batch.h")]
 _lib = None
@@ -30,7 +33,7 @@ def lib():
     if _lib is None:
         if not os.path.exists(OUT) or any(os.path.getmtime(d) > os.path.getmtime(OUT) for d in DEPS):
             os.makedirs(os.path.dirname(OUT), exist_ok=True)
-            subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O2", "-std=c++17", "-fPIC",
+            subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O2", "-std=c++17", "-fPIC", *DEFS,
                             "-shared", "-o", OUT, SRC], check=True)
         _lib = C.CDLL(OUT)
     return _lib
@@ -121,21 +124,23 @@ def test_random_schedules(i):
     check(cfg, int(rng.integers(0, 1 << 34)), int(rng.integers(1, 800)), max_bail_frac=0.5)
 
 
-@pytest.mark.parametrize("layout", [0, 2])
+@pytest.mark.parametrize("layout", [0, 2, 3])
 @pytest.mark.parametrize("c", [3, 4])
 def test_layouts(c, layout, monkeypatch):
-    """Both link layouts (4-entry FIFOs, and the compact 2-entry FIFOs with the
-    reply seq packed beside the request FIFO) on the short-delay configs."""
+    """Every link layout (4-entry FIFOs; the compact 3-entry FIFOs with the
+    reply seq packed beside the request FIFO, on the 8- and on the 4-step
+    timing wheel) on the short-delay configs."""
     monkeypatch.setenv("EV_LAYOUT", str(layout))
     _, _, bails = check(pxb.CONFIGS[c], 5000, 2000, max_bail_frac=0.03)
     if layout == 0:
         assert len(bails) == 0
 
 
+@pytest.mark.parametrize("layout", [2, 3])
 @pytest.mark.parametrize("P", [1, 2, 3])
 @pytest.mark.parametrize("N", [2, 5, 9])
-def test_compact_layout_topologies(P, N, monkeypatch):
-    monkeypatch.setenv("EV_LAYOUT", "2")
+def test_compact_layout_topologies(P, N, layout, monkeypatch):
+    monkeypatch.setenv("EV_LAYOUT", str(layout))
     cfg = pxb.Config(seed=0x77 + 16 * P + N, n_proposers=P, n_acceptors=N, loss_ppm=100000,
                      delay_max=4, skew_max=2, crash_ppm=150000, crash_len_max=8,
                      crash_start_max=6, step_cap=300)

@@ -93,6 +93,26 @@ def test_log_mode_matches_oracle(gpu_lib, P, N, loss, delay, ticks, period, cras
     assert cnt["executes"] >= cnt["decided"]
 
 
+@pytest.mark.parametrize("P,loss,crash,period,delay,clen", [(1, 10000, 150000, 8, 2, 20), (2, 0, 100000, 12, 1, 30)])
+def test_log_mode_past_log_track(gpu_lib, P, loss, crash, period, delay, clen):
+    """Faulty log mode with 100 Ticks per proposer: logs grow past LOG_TRACK = 32
+    positions (SEMANTICS §7, §9).  LOG_TRUNC, LOG_DIVERGENCE (checked over the
+    first 32 positions only), the digests of the whole logs and the log lengths
+    equal the oracle's, instance by instance; the batch holds truncated
+    instances, divergent ones, and truncated divergent ones."""
+    cfg = pxb.Config(seed=0x7A0C + P, n_proposers=P, n_acceptors=5, loss_ppm=loss, delay_max=delay, skew_max=2,
+                     crash_ppm=crash, crash_len_max=clen, crash_start_max=400 if P == 1 else 600, step_cap=2048,
+                     n_ticks=100, tick_period=period)
+    res, cnt = _cmp(cfg, 11, 3000)
+    flags = res[:, 3] & 0xFF
+    trunc = (flags & pxb.F_LOG_TRUNC) != 0
+    div = (flags & pxb.F_LOG_DIVERGENCE) != 0
+    assert cnt["log_trunc"] == int(trunc.sum()) > 0 and cnt["divergence"] == int(div.sum())
+    assert trunc.sum() > 100 and div.sum() > 0 and (trunc & div).sum() > 0, (trunc.sum(), div.sum())
+    _, _, acc, _ = pxb.run(cfg, 11, 200, want_acceptors=True)
+    assert ((acc[:, :, 3] & 0x7FFFFFFF) > 32).any()
+
+
 @pytest.mark.parametrize("n", [1 << 20, 1 << 25])
 def test_log_mode_full_size_properties(gpu_lib, n):
     """Fault-free log mode: every one of the 8 Ticks commits its own command,

@@ -18,6 +18,8 @@ struct HostMem {
   void st(uint32_t i, uint32_t v) const { w[i] = v; }
   uint32_t ld16(uint32_t base, uint32_t i) const { return reinterpret_cast<const uint16_t*>(w + base)[i]; }
   void st16(uint32_t base, uint32_t i, uint32_t v) const { reinterpret_cast<uint16_t*>(w + base)[i] = (uint16_t)v; }
+  uint32_t ld16h(uint32_t i, uint32_t half) const { return reinterpret_cast<const uint16_t*>(w + i)[half]; }
+  void st16h(uint32_t i, uint32_t half, uint32_t v) const { reinterpret_cast<uint16_t*>(w + i)[half] = (uint16_t)v; }
   void orw(uint32_t i, uint32_t v) const { w[i] |= v; }
 };
 
