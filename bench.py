@@ -366,6 +366,27 @@ def north_star_line(rank, world, stream=None, dev=None, dry_total=0):
     return line
 
 
+def log_faulty_line(stream, dev, n=1 << 20):
+    """Faulty log mode (pxb.LOG_FAULTY_CONFIG: P = 2, N = 5, 10 % loss, delays
+    to 4, crash windows, 16 Ticks 8 steps apart) on the per-lane kernel's
+    log-mode shape, and the same batch on the general kernel (PXB_NO_EV=1) for
+    the speed-up; the totals of the two must be identical."""
+    import pxb
+    cfg = pxb.LOG_FAULTY_CONFIG
+    es, ek, ecnt = run_workload(GpuLeg(cfg, n, 0, 1, stream, dev), n, 2, 1, 1)
+    os.environ["PXB_NO_EV"] = "1"
+    try:
+        gs, gk, gcnt = run_workload(GpuLeg(cfg, n, 0, 1, stream, dev), n, 2, 1, 1)
+    finally:
+        del os.environ["PXB_NO_EV"]
+    assert gcnt == ecnt, (gcnt, ecnt)
+    return {"workload": "faulty log mode: P=2, N=5, 10% loss, delay [1,4], crash windows, 16 Ticks / 8 steps",
+            "instances_per_step": n, "instances_per_s": ecnt["instances"] / es,
+            "commands_committed_per_s": ecnt["executes"] / es, "kernel_ms": ek,
+            "general_kernel": {"instances_per_s": gcnt["instances"] / gs, "kernel_ms": gk},
+            "speedup_vs_general_kernel": gk / ek, "counters": ecnt}
+
+
 def dry_main(args, rank, world):
     """--dry-run: the N-rank launcher path on CPU (gloo); prints the JSON line
     shape with a synthetic workload and "data": "dry-run" (not a measurement)."""
@@ -463,6 +484,7 @@ def main():
         extra["log_mode"] = {"instances_per_step": en, "ticks_per_proposer": pxb.LOG_CONFIG.n_ticks,
                              "commands_committed_per_s": ecnt["executes"] / es,
                              "instances_per_s": ecnt["instances"] / es, "kernel_ms": ek, "counters": ecnt}
+        extra["log_mode_faulty"] = log_faulty_line(stream, dev)
         line["extra"] = extra
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)

@@ -120,17 +120,17 @@ __global__ __launch_bounds__(TCOPIES) void finalize_kernel(unsigned long long* p
 typedef void (*kernel_ptr)(KParams);
 typedef void (*ev_kernel_ptr)(ev::EvKParams);
 
-template <int PM, int W, bool C>
+template <int PM, int W, bool C, bool L = false>
 static ev_kernel_ptr ev_pick_n(uint32_t n) {
   switch (n) {
-    case 2: return ev::paxos_ev_kernel<PM, 2, W, C>;
-    case 3: return ev::paxos_ev_kernel<PM, 3, W, C>;
-    case 4: return ev::paxos_ev_kernel<PM, 4, W, C>;
-    case 5: return ev::paxos_ev_kernel<PM, 5, W, C>;
-    case 6: return ev::paxos_ev_kernel<PM, 6, W, C>;
-    case 7: return ev::paxos_ev_kernel<PM, 7, W, C>;
-    case 8: return ev::paxos_ev_kernel<PM, 8, W, C>;
-    case 9: return ev::paxos_ev_kernel<PM, 9, W, C>;
+    case 2: return ev::paxos_ev_kernel<PM, 2, W, C, L>;
+    case 3: return ev::paxos_ev_kernel<PM, 3, W, C, L>;
+    case 4: return ev::paxos_ev_kernel<PM, 4, W, C, L>;
+    case 5: return ev::paxos_ev_kernel<PM, 5, W, C, L>;
+    case 6: return ev::paxos_ev_kernel<PM, 6, W, C, L>;
+    case 7: return ev::paxos_ev_kernel<PM, 7, W, C, L>;
+    case 8: return ev::paxos_ev_kernel<PM, 8, W, C, L>;
+    case 9: return ev::paxos_ev_kernel<PM, 9, W, C, L>;
   }
   return nullptr;
 }
@@ -169,21 +169,25 @@ static ffp_kernel_ptr ffp_pick(uint32_t p, uint32_t n) {
   return p == 1 ? ffp_pick_n<1>(n) : p == 2 ? ffp_pick_n<2>(n) : p == 3 ? ffp_pick_n<3>(n) : nullptr;
 }
 
-// layout index: 0 = 8-step wheel, 1 = 16-step wheel, 2 / 3 = compact links (8- / 4-step wheel)
+// layout index: 0 = 8-step wheel, 1 = 16-step wheel, 2 / 3 = compact links (8- / 4-step wheel),
+// 4 = log mode (8-step wheel)
 static ev_kernel_ptr ev_pick(uint32_t pm, uint32_t n, int layout) {
   switch (pm * 10 + (uint32_t)layout) {
     case 10: return ev_pick_n<1, 8, false>(n);
     case 11: return ev_pick_n<1, 16, false>(n);
     case 12: return ev_pick_n<1, 8, true>(n);
     case 13: return ev_pick_n<1, 4, true>(n);
+    case 14: return ev_pick_n<1, 8, false, true>(n);
     case 20: return ev_pick_n<2, 8, false>(n);
     case 21: return ev_pick_n<2, 16, false>(n);
     case 22: return ev_pick_n<2, 8, true>(n);
     case 23: return ev_pick_n<2, 4, true>(n);
+    case 24: return ev_pick_n<2, 8, false, true>(n);
     case 30: return ev_pick_n<3, 8, false>(n);
     case 31: return ev_pick_n<3, 16, false>(n);
     case 32: return ev_pick_n<3, 8, true>(n);
     case 33: return ev_pick_n<3, 4, true>(n);
+    case 34: return ev_pick_n<3, 8, false, true>(n);
   }
   return nullptr;
 }
@@ -276,7 +280,7 @@ struct EvLists {
 };
 static EvLists g_lists[64][EV_LIST_STREAMS];
 static int g_nlists[64], g_lnext[64];
-static int g_eocc[4][4][10][64];
+static int g_eocc[5][4][10][64];
 static int g_ff1occ[10][64];
 static int g_ffpocc[4][10][64];
 
@@ -458,7 +462,8 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
   // to 12: 347 vs 689; P = 2, N = 9, delays to 12: 97 vs 247).
   // PXB_NO_EV=1 forces the general kernel.
   const char* no_ev = getenv("PXB_NO_EV");
-  bool use_ev = !ff && !logm && ev::eligible(cfg) && !(no_ev && atoi(no_ev) > 0);
+  // (faulty log mode too: the per-lane kernel's log-mode fields, 8-step wheel)
+  bool use_ev = !ff && ev::eligible(cfg) && !(no_ev && atoi(no_ev) > 0);
   // tests: a smaller bailed-id list, to exercise its overflow path
   const char* cap_s = getenv("PXB_EV_BAIL_CAP");
   const uint32_t bail_cap = (cap_s && atoi(cap_s) >= 0) ? std::min<uint32_t>((uint32_t)atoi(cap_s), EV_BAIL_CAP)

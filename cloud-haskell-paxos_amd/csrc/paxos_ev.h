@@ -66,10 +66,11 @@ static_assert(MAX_STEP_CAP < PXB_TICKET_LIMIT, "EV tickets never reach the overf
 // lane modes
 constexpr uint32_t M_IDLE = 0, M_RUN = 1;
 
-template <int PM_, int N_, int POOL_, int W_, bool CMP_>
+template <int PM_, int N_, int POOL_, int W_, bool CMP_, bool LG_ = false>
 struct Shape {
   static constexpr int PM = PM_, N = N_, POOL = POOL_, W = W_;
   static constexpr bool CMP = CMP_;                  // compact links (see Layouts)
+  static constexpr bool LG = LG_;                    // log mode (several Ticks, long logs; see Layouts)
   static constexpr int NLQ = PM * N;                 // request (and response) links
   static constexpr int NIN = PM * (N + 1);           // proposer-input bits (Tick + N links each)
   static constexpr int WW = (NLQ + NIN <= 32) ? 1 : 2;   // wheel words per slot
@@ -90,8 +91,13 @@ struct Shape {
   // hold more than 4 broadcasts of one proposer in flight (BASELINE configs
   // 3 and 4: the bail rate is the same with 4 slots as with 8)
   static constexpr uint32_t BR = CMP ? 4 : 8;
-  static constexpr int BRING = POOLW + POOL;         // PM*BR halfwords: broadcast payloads
-  static constexpr int WHEEL = BRING + PM * BR / 2;  // W * WW due masks
+  // log mode: the responses' 14-bit commands in a halfword array beside the
+  // pool (+ one dummy halfword), the first LOG_TRACK positions of the
+  // canonical log (halfwords), 32-bit broadcast payloads
+  static constexpr int POOLZ = POOLW + POOL;         // LG: POOL + 1 halfwords
+  static constexpr int BRING = POOLZ + (LG ? POOL / 2 + 1 : 0);   // PM*BR payloads: halfwords (LG: words)
+  static constexpr int CLOG = BRING + (LG ? PM * BR : PM * BR / 2);   // LG: PXB_LOG_TRACK halfwords
+  static constexpr int WHEEL = CLOG + (LG ? PXB_LOG_TRACK / 2 : 0);   // W * WW due masks
   static constexpr int WORDS = WHEEL + W * WW;
   static_assert(W == 4 || W == 8 || W == 16, "wheel of 4, 8 or 16 steps");
   static_assert(NIN <= 32 && NLQ <= 32, "masks are 32-bit");
@@ -109,6 +115,13 @@ struct Shape {
 //   broadcast payload   x [11:0] | z [13:12] | kind [15:14]
 //   acceptor word       t_max [11:0] | t_store [23:12] | val [25:24] | dead [26] | log_len [31:27]
 //   window              c0 [15:0] | c1 [31:16]  (clamped to 4096: steps are < 4095)
+// Log mode (LG) carries commands "c<id>.<t>" as 14 bits, id [13:12] | t [11:0]
+// (t >= 1; 0 = Nothing), so:
+//   acceptor word       t_max [11:0] | t_store [23:12] | dead [24]; a second word (accv):
+//                       the stored command [13:0] | log_len [31:14]
+//   response word       z [25:24] unused: the command in the pool's halfword array
+//   broadcast payload   x [11:0] | z [25:12] | kind [31:30], one word
+//   proposer            pw1 = mr_v [13:0] | r2_v [27:14], pw2 = the t of its own command
 // The due step of a queued response is kept in its link word only for the
 // tail (the FIFO max-chain of §5); "is the next one due now" reads the
 // response's own due nibble [29:26] (x, y < 2^12, z < 4: bits 26..29 free).
@@ -122,6 +135,7 @@ struct EvParams {
   uint32_t loss_m1, crash_m1;
   uint32_t loss_ppm, crash_ppm;
   uint32_t crash_len_max, crash_start_max, skew_max, step_cap;
+  uint32_t n_ticks, tick_period;      // log mode: Ticks per proposer (> 1) and their spacing
 };
 constexpr uint32_t EV_CFG_RANDOMIZE = 1u << 0, EV_CFG_LOSSY = 1u << 1, EV_CFG_CRASHY = 1u << 2;
 constexpr uint32_t EV_CFG_DRAWS = 1u << 3;    // some instance may draw message loss / delay
@@ -153,9 +167,11 @@ struct EvOut {
 // EARLY: a step may end with the copies of its last broadcast still to send
 // (see end_op); the trace kernel turns it off so that its per-step records
 // hold every message of the step in flight, as the oracle's do.
-template <int PM, int N, int POOL, int W, bool CMP, class Mem, bool EARLY = true>
+template <int PM, int N, int POOL, int W, bool CMP, class Mem, bool EARLY = true, bool LG = false>
 struct EvLane {
-  using S = Shape<PM, N, POOL, W, CMP>;
+  using S = Shape<PM, N, POOL, W, CMP, LG>;
+  // acceptor fields (Layouts): dead bit, log-length shift (LG: in accv) and its limit
+  static constexpr uint32_t A_DEAD = LG ? 24 : 26, A_LEN = LG ? 14 : 27, A_LEN_MAX = LG ? (1u << 18) - 1u : 31;
   using pool_mask_t = typename std::conditional<(POOL > 32), unsigned long long, uint32_t>::type;
   static constexpr uint32_t NLQ = S::NLQ;
   static constexpr uint32_t WM = (uint32_t)W - 1u;
@@ -179,12 +195,16 @@ struct EvLane {
   //   pw0 = ticket [11:0] | mr_t [23:12] | acks [27:24] | state [29:28] | pending [30]
   //   pw1 = mr_v [1:0] | r2_v [3:2] | cmd [5:4]
   uint32_t pw0[PM], pw1[PM];
-  uint32_t skew[PM];
+  uint32_t pw2[PM];                   // LG: the t of the proposer's own command (0: Nothing)
+  uint32_t skew[PM];                  // the (next) Tick step of each proposer
+  uint32_t tk_end[PM];                // LG: its last Tick step
+  uint32_t tper;                      // LG: steps between Ticks
   uint32_t nsent[PM];                 // broadcasts of p whose copies have started (request-link seq)
   uint32_t bnext[PM];                 // next broadcast-ring slot
   uint32_t refc[PM];                  // ring-slot reference counts (4-bit nibbles)
   // acceptor states (Server.hs:24-31), isolation windows, log digests
   uint32_t accw[N], win[N], accd[N];
+  uint32_t accv[LG ? N : 1];          // LG: the stored command and log length of each acceptor
   uint32_t pq, pq_len, acur;          // pending broadcasts (p << 3 | slot, 5 bits each), next acceptor
   bool pq_old;                        // the head pending broadcast was made at step s - 1
   uint32_t canon0;                    // canon on entering a step that carries one over (else canon - 1)
@@ -264,6 +284,11 @@ struct EvLane {
     set_from<K>(v, 1u << q, x);
   }
 
+  // a value as the reference's command code (id << 24) | t (SEMANTICS §2)
+  __host__ __device__ static __forceinline__ uint32_t code_of(uint32_t v) {
+    return LG ? (((v >> 12) << 24) | (v & 0xFFFu)) : ((v << 24) | 1u);
+  }
+
   // fields of the packed proposer state of p (finish, trace)
   __host__ __device__ uint32_t p_ticket(int p) const { return pw0[p] & 0xFFFu; }
   __host__ __device__ uint32_t p_mr_t(int p) const { return (pw0[p] >> 12) & 0xFFFu; }
@@ -317,7 +342,14 @@ struct EvLane {
     acc_mask = wq;
     // Ticks only up to the last skew
     uint32_t tk = 0u;
-    if (any_lane(t <= last_tick)) tk = (t <= last_tick) ? ticks_at(t) : 0u;   // (first steps only)
+    if (any_lane(t <= last_tick)) {                 // (single decree: the first steps only)
+      tk = (t <= last_tick) ? ticks_at(t) : 0u;
+      if constexpr (LG) {                            // the next Tick of each proposer that ticked
+#pragma unroll
+        for (int p = 0; p < PM; ++p)
+          skew[p] = (((tk >> (p * (N + 1))) & 1u) && skew[p] < tk_end[p]) ? skew[p] + tper : skew[p];
+      }
+    }
     in_mask = wi | tk;
 #pragma unroll
     for (int p = 0; p < PM; ++p) {
@@ -365,12 +397,16 @@ struct EvLane {
     uint4 wsk = make_uint4(0, 0, 0, 0);
     if (kp.skew_max > 0u) wsk = draw(0u, 2u << 24);
     last_tick = 0;
+    tper = kp.tick_period;
 #pragma unroll
     for (int p = 0; p < PM; ++p) {
       const uint32_t wp = (p == 0) ? wsk.x : (p == 1) ? wsk.y : wsk.z;
       skew[p] = (kp.skew_max > 0u && (uint32_t)p < P) ? mulhi_n(wp, kp.skew_max + 1u) : 0u;
-      last_tick = ((int32_t)skew[p] > last_tick) ? (int32_t)skew[p] : last_tick;
-      pw0[p] = pw1[p] = 0u;                        // ticket 0, Idle, no command (Client.hs:90-95)
+      // log mode: n_ticks Ticks tick_period apart (SEMANTICS §9)
+      tk_end[p] = LG ? skew[p] + (kp.n_ticks - 1u) * kp.tick_period : skew[p];
+      const int32_t lt = (int32_t)(((uint32_t)p < P) ? tk_end[p] : 0u);
+      last_tick = (lt > last_tick) ? lt : last_tick;
+      pw0[p] = pw1[p] = pw2[p] = 0u;               // ticket 0, Idle, no command (Client.hs:90-95)
       nsent[p] = bnext[p] = refc[p] = 0u;
     }
 #pragma unroll
@@ -387,6 +423,7 @@ struct EvLane {
       c1 = c1 < 4096u ? c1 : 4096u;
       win[a] = c0 | (c1 << 16);
       accw[a] = 0u;
+      if constexpr (LG) accv[a] = 0u;
       accd[a] = 0x811C9DC5u;
     }
 #pragma unroll
@@ -426,8 +463,13 @@ struct EvLane {
     // (non-short-circuit: || here became two exec-mask branches)
     bailed = bailed | (p0 & (((rc >> (4u * slot0)) & 15u) != 0u)) | (p1 & (((rc >> (4u * slot1)) & 15u) != 0u));
     if (p0) {                                        // (p1 only with p0)
-      m.st16h(S::BRING + bring_word(q, slot0), bring_half(q, slot0), x0 | (z0 << 12) | (kind0 << 14));
-      if (p1) m.st16h(S::BRING + bring_word(q, slot1), bring_half(q, slot1), x1 | (ASK << 14));
+      if constexpr (LG) {
+        m.st(S::BRING + q * S::BR + slot0, x0 | (z0 << 12) | (kind0 << 30));
+        if (p1) m.st(S::BRING + q * S::BR + slot1, x1 | (ASK << 30));
+      } else {
+        m.st16h(S::BRING + bring_word(q, slot0), bring_half(q, slot0), x0 | (z0 << 12) | (kind0 << 14));
+        if (p1) m.st16h(S::BRING + bring_word(q, slot1), bring_half(q, slot1), x1 | (ASK << 14));
+      }
     }
     pq |= (p0 ? ((q << 3) | slot0) << (5u * pq_len) : 0u) | (p1 ? ((q << 3) | slot1) << (5u * pq_len + 5u) : 0u);
     pq_len += (p0 ? 1u : 0u) + (p1 ? 1u : 0u);
@@ -442,6 +484,7 @@ struct EvLane {
   struct Reply {
     bool snd;
     uint32_t Lr, pw, bit;
+    uint32_t z;                       // LG: the Round1OK's command (the pool's halfword array)
   };
 
   // The iteration's first send, on draw w: the acceptor's reply on link
@@ -485,6 +528,10 @@ struct EvLane {
     // the pool word: to a free entry (harmless unless a reply goes), or, with
     // none free, to the link word, which the next store rewrites
     m.st(pfree ? S::POOLW + k2 : lw, rp.pw | (due4 << 26));
+    if constexpr (LG) {                              // (no free entry: the dummy halfword)
+      const uint32_t zi = pfree ? k2 : (uint32_t)POOL;
+      m.st16h(S::POOLZ + (zi >> 1), zi & 1u, rp.z);
+    }
     pfree &= (go & isR) ? ~((pool_mask_t)1 << k2) : ~(pool_mask_t)0;
     // (entries above a FIFO's length are 0: appends are additions)
     const uint32_t nR = ((wv + (1u << S::RL) + (k2 << (S::IB * len))) & ~(15u << S::RD)) | (due4 << S::RD);
@@ -602,18 +649,26 @@ struct EvLane {
     const bool keep = (len > 1u) & (((wq >> 10) & 15u) == s4);   // the next entry due now too
     acc_mask = (acc & !keep) ? (acc_mask & ~(1u << L)) : acc_mask;
     in_flight -= acc ? 1u : 0u;
-    const uint32_t w16 = m.ld16h(S::BRING + bring_word(p, bslot), bring_half(p, bslot));
+    uint32_t kind, x, z;
+    if constexpr (LG) {
+      const uint32_t w32 = m.ld(S::BRING + p * S::BR + bslot);
+      kind = w32 >> 30, x = w32 & 0xFFFu, z = (w32 >> 12) & 0x3FFFu;
+    } else {
+      const uint32_t w16 = m.ld16h(S::BRING + bring_word(p, bslot), bring_half(p, bslot));
+      kind = w16 >> 14, x = w16 & 0xFFFu, z = (w16 >> 12) & 3u;
+    }
     put(refc, p, get(refc, p) - (acc ? 1u << (4u * bslot) : 0u));
-    const uint32_t kind = w16 >> 14, x = w16 & 0xFFFu, z = (w16 >> 12) & 3u;
     const uint32_t A = get(accw, a);
-    const bool dead = ((A >> 26) & 1u) != 0u;
+    const bool dead = ((A >> A_DEAD) & 1u) != 0u;
     const uint32_t wa = get(win, a);                 // isolated at s: c0 <= s < c1 (SEMANTICS §4)
     const bool isol = ((wa & 0xFFFFu) <= (uint32_t)s) & ((uint32_t)s < (wa >> 16));
     const bool live = acc & !dead & !isol;
     const uint32_t rb = (kind == PROPOSE) ? 12u : 8u;
     canon += acc ? (live ? 2u * rb + 32u : rb) : 0u;
-    const uint32_t t_max = A & 0xFFFu, t_store = (A >> 12) & 0xFFFu, val = (A >> 24) & 3u;
-    uint32_t log_len = A >> 27;
+    const uint32_t t_max = A & 0xFFFu, t_store = (A >> 12) & 0xFFFu;
+    const uint32_t V = LG ? get(accv, a) : A;
+    const uint32_t val = LG ? V & 0x3FFFu : (A >> 24) & 3u;
+    uint32_t log_len = V >> A_LEN;
     const bool is_ask = live & (kind == ASK), is_prop = live & (kind == PROPOSE), is_exec = live & (kind == EXECUTE);
     const bool grant = is_ask & !(t_max >= x);                // Server.hs:56
     const bool accept = is_prop & (x == t_max);                 // :66 (equality, not >=)
@@ -629,18 +684,37 @@ struct EvLane {
     const uint32_t nval = accept ? z : (run ? 0u : val);
     lflags |= panic ? (uint32_t)PXB_F_PANIC : 0u;
     if (__builtin_expect(run, 0)) {                  // executed <>= [c]: log, digest, divergence
-      if (log_len >= 31u) bailed = true;
-      put(accd, a, fnv_u32(get(accd, a), (val << 24) | 1u));
-      if (log_len < clog_len) {
-        if (((uint32_t)(clog >> (2u * log_len)) & 3u) != val) lflags |= PXB_F_LOG_DIVERGENCE;
+      if (log_len >= A_LEN_MAX) bailed = true;
+      put(accd, a, fnv_u32(get(accd, a), code_of(val)));
+      if constexpr (LG) {                            // the canonical log's first LOG_TRACK positions (LDS)
+        if (log_len < (uint32_t)PXB_LOG_TRACK) {
+          const uint32_t cw = S::CLOG + (log_len >> 1), ch = log_len & 1u;
+          if (log_len < clog_len) {
+            if (m.ld16h(cw, ch) != val) lflags |= PXB_F_LOG_DIVERGENCE;
+          } else {
+            m.st16h(cw, ch, val);
+            clog_len += 1u;
+          }
+        } else {
+          lflags |= PXB_F_LOG_TRUNC;
+        }
       } else {
-        clog |= (unsigned long long)val << (2u * log_len);
-        clog_len += 1u;
+        if (log_len < clog_len) {
+          if (((uint32_t)(clog >> (2u * log_len)) & 3u) != val) lflags |= PXB_F_LOG_DIVERGENCE;
+        } else {
+          clog |= (unsigned long long)val << (2u * log_len);
+          clog_len += 1u;
+        }
       }
       log_len += 1u;
     }
     // (a lane without a live request rebuilds its old word unchanged)
-    put(accw, a, nt_max | (nt_store << 12) | (nval << 24) | ((dead | panic) ? (1u << 26) : 0u) | (log_len << 27));
+    if constexpr (LG) {
+      put(accw, a, nt_max | (nt_store << 12) | ((dead | panic) ? (1u << A_DEAD) : 0u));
+      put(accv, a, nval | (log_len << A_LEN));
+    } else {
+      put(accw, a, nt_max | (nt_store << 12) | (nval << 24) | ((dead | panic) ? (1u << 26) : 0u) | (log_len << 27));
+    }
     const bool snd1 = live & !is_exec;              // the reply, on link a -> p
     m.st(S::REQ + L, acc ? rq2 + ((S::CMP && snd1) ? 1u << S::KSH : 0u) : wq);
 
@@ -655,7 +729,8 @@ struct EvLane {
     if (!S::CMP) m.st16(S::RSEQ, L, snd1 ? kr + 1u : kr);
     rp.snd = snd1;
     rp.Lr = p * (uint32_t)N + a;
-    rp.pw = rx | (ry << 12) | (rz << 24) | (rk << 30);
+    rp.pw = rx | (ry << 12) | (LG ? 0u : (rz << 24)) | (rk << 30);
+    rp.z = rz;
     rp.bit = S::ISH + p * (N + 1) + 1u + a;
     return w1;
   }
@@ -683,12 +758,20 @@ struct EvLane {
       const bool rkeep = resp & (rlen > 1u) & (((pn >> 26) & 15u) == s4);
       in_mask = (pin & !rkeep) ? (in_mask & ~(1u << j)) : in_mask;
       in_flight -= resp ? 1u : 0u;
-      const uint32_t rkind = pe >> 30, px = pe & 0xFFFu, py = (pe >> 12) & 0xFFFu, pz = (pe >> 24) & 3u;
+      const uint32_t rkind = pe >> 30, px = pe & 0xFFFu, py = (pe >> 12) & 0xFFFu;
+      const uint32_t pz = LG ? m.ld16h(S::POOLZ + (k >> 1), k & 1u) : (pe >> 24) & 3u;
       canon += resp ? 2u * (16u >> rkind) : 0u;         // Round1OK 16, HaveTicket 8, Round2Success 4
 
       const uint32_t w0 = get(pw0, q), w1 = get(pw1, q);
       const uint32_t T = w0 & 0xFFFu, MT = (w0 >> 12) & 0xFFFu, K = (w0 >> 24) & 15u, R = (w0 >> 28) & 3u;
-      const uint32_t PD = (w0 >> 30) & 1u, MV = w1 & 3u, C2 = (w1 >> 2) & 3u, CM = (w1 >> 4) & 3u;
+      const uint32_t PD = (w0 >> 30) & 1u;
+      uint32_t MV, C2, CM, CT = 0u;
+      if constexpr (LG) {                            // 14-bit commands; own command c<q+1>.<CT>
+        CT = get(pw2, q);
+        MV = w1 & 0x3FFFu, C2 = (w1 >> 14) & 0x3FFFu, CM = CT ? (((q + 1u) << 12) | CT) : 0u;
+      } else {
+        MV = w1 & 3u, C2 = (w1 >> 2) & 3u, CM = (w1 >> 4) & 3u;
+      }
       uint32_t k0o = NONE, x0o = 0, z0o = 0;
       bool b1 = false;                                // the restart's AskForTicket (Client.hs:185)
       const uint32_t maj = (uint32_t)N >> 1;          // haveMajority: acks > floor(N/2), :191-194
@@ -722,10 +805,15 @@ struct EvLane {
       const uint32_t MTn = (restart | o_maj) ? 0u : (o_go ? mt : MT);
       const uint32_t MVn = (restart | o_maj) ? 0u : (o_go ? mv : MV);
       const uint32_t PDn = o_maj ? ((mv != 0u) ? 1u : 0u) : PD;
-      const uint32_t CMn = t_go ? q + 1u : (s_maj & (PD == 0u)) ? 0u : CM;
       // (without an input every field comes out unchanged)
       put(pw0, q, Tn | (MTn << 12) | (Kn << 24) | (Rn << 28) | (PDn << 30));
-      put(pw1, q, MVn | (C2n << 2) | (CMn << 4));
+      if constexpr (LG) {                            // handleTick: the command c<id>.<new ticket> (Client.hs:202-203)
+        put(pw1, q, MVn | (C2n << 14));
+        put(pw2, q, t_go ? Tn : (s_maj & (PD == 0u)) ? 0u : CT);
+      } else {
+        const uint32_t CMn = t_go ? q + 1u : (s_maj & (PD == 0u)) ? 0u : CM;
+        put(pw1, q, MVn | (C2n << 2) | (CMn << 4));
+      }
       broadcast(q, k0o, x0o, z0o, k0o != NONE, Tn, b1, C2n);
     }
   }
@@ -772,7 +860,7 @@ struct EvLane {
     for (int p = 0; p < PM; ++p)
       f |= (!capped && (uint32_t)p < P && p_state(p) != IDLE) ? (uint32_t)PXB_F_STUCK : 0u;
     canon += 16u + 4u * (uint32_t)N;
-    o.res[0] = dval ? ((dval << 24) | 1u) : 0u;
+    o.res[0] = dval ? code_of(dval) : 0u;
     o.res[1] = dval ? dtick : 0u;
     o.res[2] = rounds;
     o.res[3] = (f & 0xFFu) | (steps << 16);
@@ -782,14 +870,15 @@ struct EvLane {
   }
 
   // final per-acceptor outputs (digest, record) of an ended instance
-  __host__ __device__ uint32_t digest_of(int a) const { return fnv_u32(accd[a], accw[a] >> 27); }
+  __host__ __device__ uint32_t log_len_of(int a) const { return (LG ? accv[LG ? a : 0] : accw[a]) >> A_LEN; }
+  __host__ __device__ uint32_t digest_of(int a) const { return fnv_u32(accd[a], log_len_of(a)); }
   __host__ __device__ void record_of(int a, uint32_t r[4]) const {
     const uint32_t A = accw[a];
-    const uint32_t val = (A >> 24) & 3u;
+    const uint32_t val = LG ? accv[LG ? a : 0] & 0x3FFFu : (A >> 24) & 3u;
     r[0] = A & 0xFFFu;
     r[1] = (A >> 12) & 0xFFFu;
-    r[2] = val ? ((val << 24) | 1u) : 0u;
-    r[3] = (A >> 27) | (((A >> 26) & 1u) << 31);
+    r[2] = val ? code_of(val) : 0u;
+    r[3] = log_len_of(a) | (((A >> A_DEAD) & 1u) << 31);
   }
 };
 
@@ -797,7 +886,8 @@ struct EvLane {
 // delays inside the 16-step wheel.  Fault-free and log-mode batches keep the
 // paxos_kernel.h kernels.
 __host__ inline bool eligible(const pxb_config* c) {
-  return c->n_ticks <= 1 && c->step_cap <= MAX_STEP_CAP && c->delay_max <= 15;
+  // (log mode: the 8-step wheel layout only)
+  return c->step_cap <= MAX_STEP_CAP && c->delay_max <= (c->n_ticks > 1 ? 8u : 15u);
 }
 
 }  // namespace ev
@@ -820,6 +910,8 @@ __host__ inline EvParams make_params(const pxb_config* c) {
   p.crash_start_max = c->crash_start_max;
   p.skew_max = c->skew_max;
   p.step_cap = c->step_cap;
+  p.n_ticks = c->n_ticks > 1 ? c->n_ticks : 1u;
+  p.tick_period = c->n_ticks > 1 ? c->tick_period : 1u;
   const uint64_t lt = ev_threshold(c->loss_ppm), ct = ev_threshold(c->crash_ppm);
   p.cfg = ((c->flags & PXB_CFG_RANDOMIZE) ? EV_CFG_RANDOMIZE : 0u) | (lt ? EV_CFG_LOSSY : 0u) | (ct ? EV_CFG_CRASHY : 0u);
   if ((c->flags & PXB_CFG_RANDOMIZE) || lt || c->delay_max > 1) p.cfg |= EV_CFG_DRAWS;
@@ -849,13 +941,15 @@ __host__ inline int wheel_for(uint32_t delay_max) { return delay_max <= 8 ? 8 : 
 // Layout 3 is the compact layout with a 4-step wheel (delays up to 4: BASELINE
 // configs 3 and 4), 4 words per lane fewer.
 __host__ inline int layout_for(const pxb_config* c) {
+  if (c->n_ticks > 1) return 4;                      // log mode: 8-step wheel, 4-entry FIFOs, LG fields
   if (!(c->flags & PXB_CFG_RANDOMIZE) && c->delay_max <= 4 && c->step_cap <= 512 &&
       c->n_proposers * c->n_acceptors <= 16)
     return 3;
   return wheel_for(c->delay_max) == 8 ? 0 : 1;
 }
 __host__ inline int layout_wheel(int layout) { return layout == 1 ? 16 : layout == 3 ? 4 : 8; }
-__host__ inline bool layout_compact(int layout) { return layout >= 2; }
+__host__ inline bool layout_compact(int layout) { return layout == 2 || layout == 3; }
+__host__ inline bool layout_log(int layout) { return layout == 4; }
 
 }  // namespace ev
 }  // namespace pxb

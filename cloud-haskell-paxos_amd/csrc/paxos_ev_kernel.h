@@ -77,11 +77,11 @@ struct EvPool {
 // keeps every 32-bit sum from wrapping (an instance runs < 2^12 steps and
 // sends < 2^10 messages per step: at most 2^8 x 2^22; canonical bytes are
 // summed in 64 bits).
-constexpr int EV_NTOT = 11;
+constexpr int EV_NTOT = 12;
 constexpr uint32_t EV_FLUSH = 1u << 8;
 __device__ constexpr int tot_slot[EV_NTOT] = {PXB_C_INSTANCES, PXB_C_UNDECIDED, PXB_C_STUCK, PXB_C_PANIC,
                                               PXB_C_DIVERGENCE, PXB_C_STEP_CAP, PXB_C_ROUNDS, PXB_C_STEPS,
-                                              PXB_C_MESSAGES, PXB_C_EXECUTES, PXB_C_CANON_BYTES};
+                                              PXB_C_MESSAGES, PXB_C_EXECUTES, PXB_C_LOG_TRUNC, PXB_C_CANON_BYTES};
 
 struct EvTotals {
   uint32_t c[EV_NTOT - 1];            // the 32-bit sums, in tot_slot order
@@ -114,16 +114,16 @@ struct EvTotals {
 // The compact layout leaves room for 10 resident waves per CU (LDS), i.e. 3
 // on some SIMDs: its register budget is then 168 VGPRs, which the second
 // bound (minimum waves per SIMD) makes the compiler keep to.
-template <int PM, int N, int W, bool CMP>
+template <int PM, int N, int W, bool CMP, bool LG = false>
 __global__ __launch_bounds__(64, CMP ? 3 : 1) void paxos_ev_kernel(EvKParams kp) {
   constexpr int POOL = EvPool<PM, N, CMP>::value;
-  using S = Shape<PM, N, POOL, W, CMP>;
+  using S = Shape<PM, N, POOL, W, CMP, LG>;
   __shared__ uint32_t lds[S::WORDS * 64];
   const uint32_t lane = threadIdx.x;
   unsigned long long* const trow = kp.part + (size_t)(blockIdx.x % EV_TCOPIES) * 16u;
   EvTotals tot;
   tot.clear();
-  EvLane<PM, N, POOL, W, CMP, LdsMem> L;
+  EvLane<PM, N, POOL, W, CMP, LdsMem, true, LG> L;
   L.m = LdsMem{lds, lane};
   L.set_keys(kp.p);
   L.mode = M_IDLE;
@@ -192,6 +192,7 @@ __global__ __launch_bounds__(64, CMP ? 3 : 1) void paxos_ev_kernel(EvKParams kp)
         tot.c[7] += o.steps;
         tot.c[8] += L.msgs;
         tot.c[9] += L.execs;
+        if (LG) tot.c[10] += (f & PXB_F_LOG_TRUNC) ? 1u : 0u;
         tot.canon += L.canon;
         if (kp.out) kp.out[L.gid] = make_uint4(o.res[0], o.res[1], o.res[2], o.res[3]);
         if (kp.dig) {

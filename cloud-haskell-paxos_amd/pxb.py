@@ -151,6 +151,12 @@ CONFIG_INSTANCES = {1: 1 << 10, 2: 1 << 20, 3: 1 << 24, 4: 1 << 26, 5: 1 << 28}
 LOG_CONFIG = Config(seed=0x5EED0006, n_proposers=2, n_acceptors=2, step_cap=1024,
                     n_ticks=16, tick_period=8)
 CONFIGS[6] = LOG_CONFIG
+# Faulty log mode: config 3's duel and loss with crash windows, 16 Ticks per
+# proposer (the per-lane kernel's log-mode shape; bench.py extra.log_mode_faulty)
+LOG_FAULTY_CONFIG = Config(seed=0x5EED0007, n_proposers=2, n_acceptors=5, loss_ppm=100000, delay_max=4,
+                           skew_max=3, crash_ppm=200000, crash_len_max=16, crash_start_max=64, step_cap=1024,
+                           n_ticks=16, tick_period=8)
+CONFIGS[7] = LOG_FAULTY_CONFIG
 
 
 def canonical_bytes_nofault(n_acceptors: int) -> int:

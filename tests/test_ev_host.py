@@ -178,3 +178,50 @@ def test_split_shape_config5(first, monkeypatch):
     p3 = np.nonzero(drawn == 3)[0]
     assert set(p3.tolist()) <= set(bails.tolist())
     assert len(bails) - len(p3) <= 0.02 * 1500
+
+
+# ---- log mode (docs/SEMANTICS.md §9) on the per-lane state machine's log-mode
+# fields: periodic Ticks, 14-bit commands "c<id>.<t>", logs past LOG_TRACK ----
+@pytest.mark.parametrize("P,N,loss,delay,ticks,period,crash", [
+    (1, 5, 0, 1, 8, 6, 0),
+    (1, 3, 0, 1, 6, 2, 0),
+    (2, 5, 50000, 3, 6, 9, 0),
+    (3, 7, 150000, 4, 5, 20, 150000),
+    (2, 9, 0, 6, 12, 5, 300000),
+    (3, 4, 300000, 8, 16, 3, 0),
+    (2, 2, 0, 1, 16, 8, 0),              # the stock Main.hs topology, fault-free
+    (2, 5, 100000, 4, 16, 4, 200000)])   # BASELINE-like faulty log mode
+def test_log_mode(P, N, loss, delay, ticks, period, crash):
+    cfg = pxb.Config(seed=0x1060 + 16 * P + N, n_proposers=P, n_acceptors=N, loss_ppm=loss,
+                     delay_max=delay, skew_max=3, crash_ppm=crash, crash_len_max=12,
+                     crash_start_max=30, step_cap=1024, n_ticks=ticks, tick_period=period)
+    _, cnt, _ = check(cfg, 321, 1500, max_bail_frac=0.05)
+    assert cnt["executes"] >= cnt["decided"]
+
+
+@pytest.mark.parametrize("P,loss,crash,period,delay,clen", [(1, 10000, 150000, 8, 2, 20), (2, 0, 100000, 12, 1, 30)])
+def test_log_mode_past_log_track(P, loss, crash, period, delay, clen):
+    """100 Ticks per proposer: logs past LOG_TRACK = 32 set LOG_TRUNC; the
+    divergence check covers the first 32 positions (as the oracle's)."""
+    cfg = pxb.Config(seed=0x7A0C + P, n_proposers=P, n_acceptors=5, loss_ppm=loss, delay_max=delay, skew_max=2,
+                     crash_ppm=crash, crash_len_max=clen, crash_start_max=400 if P == 1 else 600, step_cap=2048,
+                     n_ticks=100, tick_period=period)
+    res, cnt, _ = check(cfg, 11, 600, max_bail_frac=0.05)
+    assert cnt["log_trunc"] > 0 and cnt["divergence"] > 0
+
+
+@pytest.mark.parametrize("i", range(12))
+def test_random_log_mode_schedules(i):
+    rng = np.random.default_rng(0x10E7 + i)
+    cfg = pxb.Config(
+        seed=int(rng.integers(0, 1 << 63)), n_proposers=int(rng.integers(1, 4)),
+        n_acceptors=int(rng.integers(2, 10)),
+        loss_ppm=int(rng.choice([0, rng.integers(1, 400000)])),
+        delay_max=int(rng.integers(1, 9)),
+        crash_ppm=int(rng.choice([0, rng.integers(1, 600000)])),
+        crash_len_max=int(rng.integers(1, 40)), crash_start_max=int(rng.integers(0, 200)),
+        skew_max=int(rng.choice([0, rng.integers(1, 12)])),
+        step_cap=int(rng.choice([int(rng.integers(1, 64)), 512, 2048])),
+        n_ticks=int(rng.integers(2, 60)), tick_period=int(rng.integers(1, 16)),
+        randomize=bool(rng.random() < 0.3))
+    check(cfg, int(rng.integers(0, 1 << 34)), int(rng.integers(1, 500)), max_bail_frac=0.5)

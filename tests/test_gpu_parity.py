@@ -648,3 +648,53 @@ def test_trace_production_variant_matches_oracle_steps(gpu_lib, c, inst):
             carried += 1
     assert gsteps[-1] == steps[-1]
     assert list(gres) == [res.decided_val, res.decided_ticket, res.rounds, res.packed_flags()]
+
+
+@pytest.mark.parametrize("cfg", [pxb.LOG_FAULTY_CONFIG, pxb.Config(seed=0x10E, n_proposers=3, n_acceptors=9, loss_ppm=300000,
+                                                        delay_max=8, skew_max=3, crash_ppm=200000,
+                                                        crash_len_max=16, crash_start_max=16, step_cap=512,
+                                                        randomize=True, n_ticks=12, tick_period=6)])
+def test_log_mode_per_lane_matches_general_kernel(gpu_lib, cfg):
+    """Faulty log mode runs on the per-lane kernel's log-mode shape (bails on
+    the general LOGM kernel); the general kernel alone (PXB_NO_EV=1) and the
+    oracle give identical results, digests, acceptor records and totals."""
+    a = pxb.run(cfg, 99, 40000, want_acceptors=True)
+    os.environ["PXB_NO_EV"] = "1"
+    try:
+        b = pxb.run(cfg, 99, 40000, want_acceptors=True)
+    finally:
+        del os.environ["PXB_NO_EV"]
+    for x, y in zip(a[:3], b[:3]):
+        assert np.array_equal(x, y)
+    assert a[3] == b[3]
+    _cmp(cfg, 99, 4000)
+
+
+# ---- hand-derived step-schedule KATs (tests/golden/kat_step_schedule.json) ----
+_STEP_KATS = __import__("json").load(open(os.path.join(GOLDEN, "kat_step_schedule.json")))["cases"]
+
+
+@pytest.mark.parametrize("case", _STEP_KATS, ids=[c["name"] for c in _STEP_KATS])
+@pytest.mark.parametrize("production", [False, True])
+def test_step_kats_on_gpu(gpu_lib, case, production):
+    """The GPU result, acceptor records and per-step trace (both variants of
+    the per-lane state machine) equal the hand-derived trace."""
+    import bisect
+    cfg = pxb.Config(**case["config"])
+    want = case["result"]
+    res, dig, acc, cnt = pxb.run(cfg, case["instance"], 1, want_acceptors=True)
+    assert list(res[0]) == [want["decided_val"], want["decided_ticket"], want["rounds"],
+                            want["flags"] | (want["steps"] << 16)]
+    assert (cnt["messages"], cnt["canon_bytes"], cnt["executes"]) == \
+        (want["messages"], want["canon_bytes"], want["executes"])
+    recs, tres = pxb.trace_instance(cfg, case["instance"], production=production)
+    assert list(tres) == list(res[0])
+    steps = [r["step"] for r in recs]
+    for cp in case["checkpoints"]:
+        r = recs[bisect.bisect_right(steps, cp["step"]) - 1]
+        assert [[int(x) for x in a] for a in r["acc"]] == cp["acc"], cp["step"]
+        assert [[int(x) for x in p[:4]] for p in r["prop"]] == cp["prop"], cp["step"]
+        if "in_flight" in cp and r["in_flight"] != pxb.TRACE_IN_FLIGHT_UNKNOWN:
+            assert r["in_flight"] == cp["in_flight"], cp["step"]
+    final = [cp for cp in case["checkpoints"] if cp["step"] == want["steps"] - 1][0]
+    assert acc[0].tolist() == final["acc"]

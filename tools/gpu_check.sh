@@ -13,5 +13,5 @@ print("headline %.2f G/s" % (j["value"] / 1e9))
 ns = j["north_star"]; print("north star %.2f M/s (%.1f ms)" % (ns["instances_per_s"] / 1e6, ns["ms_per_step"]))
 for k, v in j.get("extra", {}).items():
     if "instances_per_s" in v:
-        print("%s %.2f M/s" % (k, v["instances_per_s"] / 1e6))
+        print("%s %.2f M/s%s" % (k, v["instances_per_s"] / 1e6, (" (x%.2f vs general kernel)" % v["speedup_vs_general_kernel"]) if "speedup_vs_general_kernel" in v else ""))
 PY
