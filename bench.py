@@ -44,6 +44,7 @@ HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip
 CUS = 256
 VALU_PEAK_G = CUS * 2 * 2.4  # G wave64 VALU instructions / s (1228.8)
 PROFILES = os.path.join(ROOT, "profiles")
+PROFILE_ROUNDS = ("r03", "r02")   # the newest committed profile set of a workload wins
 BATCHES_PER_STEP = 256       # config-2 batches of 2^20 per timed step (>= 100 ms over 20 steps)
 DRY_NORTH_STAR = 1 << 12     # --dry-run stand-in for the north star's 2^26 total
 
@@ -53,7 +54,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5])
+    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5, 6, 7],
+                    help="BASELINE config (6: log mode, 7: faulty log mode)")
     ap.add_argument("--instances", type=int, default=0, help="per GPU per step (default: the config's step size)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
@@ -189,14 +191,16 @@ def counters_dict(v):
 
 
 def step_profile(workload: str):
-    """The committed rocprofv3 profile of this workload (tools/profile_r02.sh
+    """The committed rocprofv3 profile of this workload (tools/profile_set.sh
     + tools/roofline.py): PMC counts per instance processed, or None."""
-    path = os.path.join(PROFILES, "r02_%s" % workload, "step.json")
-    try:
-        with open(path) as f:
-            return json.load(f), path
-    except (OSError, ValueError):
-        return None, path
+    for rnd in PROFILE_ROUNDS:
+        path = os.path.join(PROFILES, "%s_%s" % (rnd, workload), "step.json")
+        try:
+            with open(path) as f:
+                return json.load(f), path
+        except (OSError, ValueError):
+            continue
+    return None, path
 
 
 def roofline(workload, n, kms, canon_bytes_per_step):
@@ -383,6 +387,7 @@ def log_faulty_line(stream, dev, n=1 << 20):
     return {"workload": "faulty log mode: P=2, N=5, 10% loss, delay [1,4], crash windows, 16 Ticks / 8 steps",
             "instances_per_step": n, "instances_per_s": ecnt["instances"] / es,
             "commands_committed_per_s": ecnt["executes"] / es, "kernel_ms": ek,
+            "roofline": roofline("config7", n, ek, ecnt["canon_bytes"] / 2),
             "general_kernel": {"instances_per_s": gcnt["instances"] / gs, "kernel_ms": gk},
             "speedup_vs_general_kernel": gk / ek, "counters": ecnt}
 

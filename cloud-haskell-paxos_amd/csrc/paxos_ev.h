@@ -82,6 +82,14 @@ struct Shape {
   static constexpr int KSH = QL + QLB, KB = 32 - KSH;
   // response FIFO: RC pool indices of IB bits, length at RL (RLB bits), tail due at RD
   static constexpr int RC = 4, RL = IB * RC, RLB = 3, RD = RL + RLB;
+  // compact layouts with a pool of <= 24 words: a Round2Success (no payload)
+  // takes no pool word; its FIFO entry is the code RCB + (due & 7) instead
+#ifdef PXB_EV_NO_RCODE
+  static constexpr bool RCODE = false;               // (A/B: every response takes a pool word)
+#else
+  static constexpr bool RCODE = CMP && POOL <= 24 && IB == 5;
+#endif
+  static constexpr uint32_t RCB = 24;
   // LDS word offsets
   static constexpr int REQ = 0;                      // NLQ: request links, index a*PM + p (CMP: + reply seq)
   static constexpr int RSEQ = REQ + NLQ;             // !CMP: NLQ halfwords of reply seq, index a*PM + p
@@ -111,6 +119,8 @@ struct Shape {
 //                       (a, p) pair in [31:23], one word for both; else 4 entries, len
 //                       [30:28], reply seq in its own halfword)
 //   response-link word  pool index i (IB bits at IB*i); len [4IB+2:4IB]; last due&15 above it
+//                       (compact, pool <= 24: index 24 + (due & 7) = a Round2Success, no
+//                       pool word; dues stay within s + delay_max <= s + 4)
 //   response word       x [11:0] | y [23:12] | z [25:24] | kind [31:30]
 //   broadcast payload   x [11:0] | z [13:12] | kind [15:14]
 //   acceptor word       t_max [11:0] | t_store [23:12] | val [25:24] | dead [26] | log_len [31:27]
@@ -522,7 +532,9 @@ struct EvLane {
     const uint32_t rel = (tail - b4) & (len ? 15u : 0u);
     const uint32_t due_rel = d > rel ? d : rel;
     const uint32_t due4 = (b4 + due_rel) & 15u;
-    bailed = bailed | (go & (isR ? (len >= (uint32_t)S::RC) | (pfree == 0) : (len >= (uint32_t)S::QC)));
+    // (a Round2Success in a compact link word needs no pool word)
+    const bool r2c = S::RCODE & isR & ((rp.pw >> 30) == R2S);
+    bailed = bailed | (go & (isR ? (len >= (uint32_t)S::RC) | ((pfree == 0) & !r2c) : (len >= (uint32_t)S::QC)));
     const uint32_t k2 = (POOL > 32) ? (uint32_t)__builtin_ctzll((unsigned long long)pfree | (1ull << 63))
                                     : ctz32((uint32_t)pfree) & 31u;
     // the pool word: to a free entry (harmless unless a reply goes), or, with
@@ -532,9 +544,10 @@ struct EvLane {
       const uint32_t zi = pfree ? k2 : (uint32_t)POOL;
       m.st16h(S::POOLZ + (zi >> 1), zi & 1u, rp.z);
     }
-    pfree &= (go & isR) ? ~((pool_mask_t)1 << k2) : ~(pool_mask_t)0;
+    pfree &= (go & isR & !r2c) ? ~((pool_mask_t)1 << k2) : ~(pool_mask_t)0;
+    const uint32_t ent = r2c ? S::RCB + (due4 & 7u) : k2;
     // (entries above a FIFO's length are 0: appends are additions)
-    const uint32_t nR = ((wv + (1u << S::RL) + (k2 << (S::IB * len))) & ~(15u << S::RD)) | (due4 << S::RD);
+    const uint32_t nR = ((wv + (1u << S::RL) + (ent << (S::IB * len))) & ~(15u << S::RD)) | (due4 << S::RD);
     const uint32_t nQ = wv + (1u << S::QL) + ((cslot | (due4 << 3)) << (7u * len));
     m.st(lw, go ? (isR ? nR : nQ) : wv);
     put(refc, cp, get(refc, cp) + ((go & !isR) ? 1u << (4u * cslot) : 0u));
@@ -749,13 +762,17 @@ struct EvLane {
       const uint32_t Lr = q * (uint32_t)N + (resp ? ra : 0u);
       const uint32_t rr = rsp_ld(Lr);
       const uint32_t rlen = (rr >> S::RL) & RLM;
-      const uint32_t k = rr & IM;
-      const uint32_t pe = m.ld(S::POOLW + k);
-      const uint32_t pn = m.ld(S::POOLW + ((rr >> S::IB) & IM));
-      pfree |= resp ? ((pool_mask_t)1 << k) : (pool_mask_t)0;
+      const uint32_t k = rr & IM, nk = (rr >> S::IB) & IM;
+      // (a Round2Success code: no pool word, its due in the code)
+      const bool kc = S::RCODE & (k >= S::RCB), nkc = S::RCODE & (nk >= S::RCB);
+      const uint32_t pe0 = m.ld(S::POOLW + (kc ? 0u : k));
+      const uint32_t pn = m.ld(S::POOLW + (nkc ? 0u : nk));
+      const uint32_t pe = kc ? (R2S << 30) : pe0;
+      pfree |= (resp & !kc) ? ((pool_mask_t)1 << k) : (pool_mask_t)0;
       m.st(S::RSP + Lr, resp ? ((rr & ((1u << S::RL) - 1u)) >> S::IB) + ((rr & ~((1u << S::RL) - 1u)) - (1u << S::RL))
                              : rr);                         // (popped: entries down one, length - 1)
-      const bool rkeep = resp & (rlen > 1u) & (((pn >> 26) & 15u) == s4);
+      const bool nnow = nkc ? ((nk & 7u) == (s4 & 7u)) : (((pn >> 26) & 15u) == s4);
+      const bool rkeep = resp & (rlen > 1u) & nnow;
       in_mask = (pin & !rkeep) ? (in_mask & ~(1u << j)) : in_mask;
       in_flight -= resp ? 1u : 0u;
       const uint32_t rkind = pe >> 30, px = pe & 0xFFFu, py = (pe >> 12) & 0xFFFu;

@@ -143,7 +143,7 @@ CONFIGS = {
               delay_max=8, crash_ppm=200000, crash_len_max=16, crash_start_max=16,
               skew_max=3, step_cap=512, randomize=True),
 }
-CONFIG_INSTANCES = {1: 1 << 10, 2: 1 << 20, 3: 1 << 24, 4: 1 << 26, 5: 1 << 28}
+CONFIG_INSTANCES = {1: 1 << 10, 2: 1 << 20, 3: 1 << 24, 4: 1 << 26, 5: 1 << 28, 6: 1 << 20, 7: 1 << 20}
 
 # Log mode (docs/SEMANTICS.md §9): the stock app/Main.hs
 # topology (2 proposers, 2 acceptors, Main.hs:41-46) with the ticker running

@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round-2 profile set of one bench workload: kernel-trace stats, one SQ/GRBM
+# Profile set of one bench workload (rounds 2, 3): kernel-trace stats, one SQ/GRBM
 # PMC pass, FETCH_SIZE and WRITE_SIZE passes (each its own run, per the
 # MI355X guide), then tools/roofline.py -> <outdir>/step.json (what bench.py
 # reads for its roofline).  Runs on the GPU box:
-#   bash tools/profile_r02.sh <outdir> <config> <instances/step> <steps> <warmup>
+#   bash tools/profile_set.sh <outdir> <config> <instances/step> <steps> <warmup>
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/$1; C=$2; NI=$3; S=$4; W=$5

@@ -22,7 +22,7 @@ from collections import defaultdict
 CUS = 256
 PEAK_CLOCK_HZ = 2.4e9
 VALU_PER_CU_CYCLE = 2.0
-KERNEL_TAGS = ("paxos_ev_kernel", "paxos_ff1_kernel", "paxos_ffp_kernel", "paxos_evl_kernel",
+KERNEL_TAGS = ("paxos_ev_kernel", "paxos_ff1_kernel", "paxos_ffp_kernel",
                "paxos_batch_kernel", "finalize_kernel")
 # kernels a profiled bench command may also run that are not part of a step
 # (torch's own fills and copies, the wire codec's passes)

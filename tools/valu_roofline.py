@@ -1,5 +1,5 @@
 """VALU-issue roofline of the batch kernel from a rocprofv3 --pmc pass
-(tools/profile_round.sh, valu/) and the kernel-trace average duration.
+(a round-1 profile directory, valu/ pass) and the kernel-trace average duration.
 
 The batch kernel keeps the protocol state on chip, so its real limiter is
 VALU issue, not HBM.  A wave64 VALU instruction issues in 2 cycles on a
