@@ -149,9 +149,6 @@ struct EvParams {
 };
 constexpr uint32_t EV_CFG_RANDOMIZE = 1u << 0, EV_CFG_LOSSY = 1u << 1, EV_CFG_CRASHY = 1u << 2;
 constexpr uint32_t EV_CFG_DRAWS = 1u << 3;    // some instance may draw message loss / delay
-// the acceptor look-ahead (EvLane::LA) may run: its replies fall due up to
-// s + 1 + delay_max, inside the wheel when delay_max + 2 <= W
-constexpr uint32_t EV_CFG_LA = 1u << 4;
 
 __host__ __device__ inline uint64_t ev_threshold(uint32_t ppm) {
   return ((((uint64_t)ppm) << 32) + 999999ull) / 1000000ull;
@@ -190,25 +187,6 @@ struct EvLane {
   static constexpr uint32_t WM = (uint32_t)W - 1u;
   static constexpr uint32_t QLM = (1u << S::QLB) - 1u, RLM = (1u << S::RLB) - 1u;
   static constexpr uint32_t IM = (1u << S::IB) - 1u;
-  // Acceptor look-ahead (LA): once every request due at s is handled, the
-  // acceptor op takes requests due at s + 1 while the proposers finish s (see
-  // acc_op).  Its replies fall due up to s + 1 + delay_max, so it needs the
-  // 8-step wheel and delay_max <= 6 (EV_CFG_LA); on that wheel (delay_max <= 8)
-  // a due is at most 9 steps past its send step's, which send_first's 4-bit
-  // relative dues hold.
-#ifdef PXB_EV_NO_LA
-  static constexpr bool LA = false;
-#else
-  static constexpr bool LA = EARLY && W == 8;
-#endif
-  static constexpr uint32_t REQ_BITS = (NLQ >= 32) ? ~0u : (1u << NLQ) - 1u;
-  // request-link bits a*PM + p of the proposers p <= q
-  __host__ __device__ static constexpr uint32_t low_props(int q) {
-    uint32_t r = 0u;
-    for (int a = 0; a < N; ++a)
-      for (int p = 0; p <= q; ++p) r |= 1u << (a * PM + p);
-    return r;
-  }
 
   Mem m;
   uint32_t rk[20];                    // Philox round keys (set_keys): uniform, held in VGPRs
@@ -220,8 +198,6 @@ struct EvLane {
   bool lossy;
   int32_t s, last_tick;
   uint32_t acc_mask;                  // this step's request links with due messages left
-  uint32_t la_mask;                   // LA: request links with messages due at s + 1 left
-  bool la_any;                        // LA: this step took requests of s + 1
   uint32_t in_mask;                   // this step's proposer inputs left (Tick / response links)
   uint32_t occ;                       // wheel slots holding due bits
   // proposer states (ClientState, Client.hs:58-67), packed (tickets < 2^12,
@@ -357,17 +333,14 @@ struct EvLane {
   // enter step t: its due links from the wheel, its Ticks;
   // 48 canonical bytes per proposer with an input (SEMANTICS §8)
   __host__ __device__ __forceinline__ void enter(int32_t t) {
-    // (LA: the links of t that the look-ahead of t - 1 emptied are out of la_mask)
-    const bool nxt = LA & ((uint32_t)t == (uint32_t)s + 1u);
     s = t;
     pq_old = pq_len != 0u;                           // (only ever one: end_op)
-    // (a step whose requests the look-ahead of t - 1 took is never "quiet at t - 1")
-    canon0 = (pq_old & !(nxt & la_any)) ? canon : canon - 1u;
+    canon0 = pq_old ? canon : canon - 1u;
     const uint32_t slot = (uint32_t)t & WM;
     uint32_t wq, wi;
     if (S::WW == 1) {
       const uint32_t wv = m.ld(S::WHEEL + slot);
-      wq = wv & REQ_BITS;
+      wq = wv & ((1u << NLQ) - 1u);
       wi = wv >> S::ISH;
     } else {
       wq = m.ld(S::WHEEL + 2u * slot);
@@ -376,11 +349,7 @@ struct EvLane {
     }
     m.st(S::WHEEL + S::WW * slot, 0u);
     occ &= ~(1u << slot);
-    acc_mask = nxt ? la_mask : wq;
-    if constexpr (LA) {
-      la_mask = m.ld(S::WHEEL + S::WW * (((uint32_t)t + 1u) & WM)) & REQ_BITS;
-      la_any = false;
-    }
+    acc_mask = wq;
     // Ticks only up to the last skew
     uint32_t tk = 0u;
     if (any_lane(t <= last_tick)) {                 // (single decree: the first steps only)
@@ -483,9 +452,6 @@ struct EvLane {
     // general kernel (config 5 runs its P <= 2 instances here: pxb_run_device)
     bailed = P > (uint32_t)PM;
     mode = M_RUN;
-    s = 0;                                           // (enter(0) is not a look-ahead successor)
-    la_mask = 0u;
-    la_any = false;
     enter(0);
   }
 
@@ -529,7 +495,6 @@ struct EvLane {
     bool snd;
     uint32_t Lr, pw, bit;
     uint32_t z;                       // LG: the Round1OK's command (the pool's halfword array)
-    uint32_t base;                    // its send step: s, or s + 1 from the look-ahead
   };
 
   // The iteration's first send, on draw w: the acceptor's reply on link
@@ -557,24 +522,15 @@ struct EvLane {
     const bool ok = !(lossy & (w.x <= loss_m1));
     const uint32_t d = 1u + mulhi_n(w.y, dmax);
     const bool go = snd & ok;
-    // the send step: s; a carried copy's s - 1; a look-ahead reply's s + 1
-    const uint32_t base = isR ? (LA ? rp.base : (uint32_t)s) : sb;
+    const uint32_t base = isR ? (uint32_t)s : sb;   // the send step (a carried copy's is s - 1)
     const uint32_t b4 = base & 15u;
     const uint32_t Lq = ca * (uint32_t)PM + cp;
     const uint32_t lw = isR ? S::RSP + rp.Lr : S::REQ + Lq;   // the link word
     const uint32_t wv = m.ld(lw);
     const uint32_t len = isR ? (wv >> S::RL) & RLM : (wv >> S::QL) & QLM;
     const uint32_t tail = isR ? (wv >> S::RD) & 15u : (wv >> ((7u * len - 4u) & 31u)) & 15u;
-    uint32_t due_rel;
-    if constexpr (LA) {
-      // (a look-ahead reply's link may still hold a response due at s = base - 1:
-      // tail - base + 1 >= 0 on every link)
-      const uint32_t rel1 = (tail - b4 + 1u) & (len ? 15u : 0u);
-      due_rel = (d + 1u > rel1 ? d + 1u : rel1) - 1u;
-    } else {
-      const uint32_t rel = (tail - b4) & (len ? 15u : 0u);
-      due_rel = d > rel ? d : rel;
-    }
+    const uint32_t rel = (tail - b4) & (len ? 15u : 0u);
+    const uint32_t due_rel = d > rel ? d : rel;
     const uint32_t due4 = (b4 + due_rel) & 15u;
     // (a Round2Success in a compact link word needs no pool word)
     const bool r2c = S::RCODE & isR & ((rp.pw >> 30) == R2S);
@@ -601,7 +557,6 @@ struct EvLane {
     m.orw(S::WHEEL + slot * S::WW + ((S::WW == 2 && isR) ? 1u : 0u), (go & !now) ? 1u << (isR ? rp.bit : Lq) : 0u);
     occ |= (go & !now) ? (1u << slot) : 0u;
     acc_mask |= (go & now) ? (1u << Lq) : 0u;
-    if constexpr (LA) la_mask |= (go & !isR & (base + due_rel == (uint32_t)s + 1u)) ? (1u << Lq) : 0u;
     in_flight += go ? 1u : 0u;
   }
 
@@ -652,7 +607,6 @@ struct EvLane {
     m.orw(S::WHEEL + slot * S::WW, (go & !now) ? 1u << Lq : 0u);
     occ |= (go & !now) ? (1u << slot) : 0u;
     acc_mask |= (go & now) ? (1u << Lq) : 0u;
-    if constexpr (LA) la_mask |= (go & (sb + due_rel == (uint32_t)s + 1u)) ? (1u << Lq) : 0u;
     in_flight += go ? 1u : 0u;
   }
 
@@ -692,46 +646,11 @@ struct EvLane {
   }
   // (ready: acc_ready_mask(); it could be taken before this iteration's copy:
   // a request that copy makes due now belongs to an acceptor it had not reached)
-  // LA: the request links whose messages due at s + 1 the acceptors may take
-  // now.  Acceptor a takes its requests of a step by (p, seq); once every
-  // request due at s is handled (and no broadcast of s - 1 has copies left)
-  // the acceptors are done with s, and a request of proposer p due at s + 1
-  // can be handled as soon as no proposer p' < p can still send one: p' has
-  // no input left at s and no pending broadcast.  (Requests that p itself
-  // sends later queue behind it on the link, FIFO.)  Every send of step s is
-  // due at s + 1 or later and the replies of the look-ahead at s + 2 or later,
-  // so neither phase of step s sees it.
-  __host__ __device__ __forceinline__ uint32_t la_allowed() const {
-    if constexpr (PM == 1) {
-      return ~0u;
-    } else {
-      const uint32_t h = pq & ((1u << (5u * pq_len)) - 1u);   // the valid pending entries (p << 3 | slot)
-      constexpr uint32_t QB = 0x42108u;                      // bit 3 of each 5-bit entry
-      uint32_t allow = ~0u;
-#pragma unroll
-      for (int q = 0; q < PM - 1; ++q) {
-        const uint32_t grp = ((1u << (N + 1)) - 1u) << (q * (N + 1));
-        // entries of proposer q: its index in bits 3-4 (PM <= 3)
-        const uint32_t eq = (q == 0) ? (~h & ~(h >> 1) & QB) : (h & ~(h >> 1) & QB);
-        const uint32_t vq = (q == 0) ? eq & ((1u << (5u * pq_len)) - 1u) : eq;
-        const bool busy = ((in_mask & grp) | vq) != 0u;
-        allow &= busy ? low_props(q) : ~0u;
-      }
-      return allow;
-    }
-  }
   __host__ __device__ __forceinline__ uint4 acc_op(const EvParams& kp, bool act, uint2 cc, Reply& rp,
                                                    uint32_t ready) {
-    uint32_t use = ready, as = (uint32_t)s;             // the request set and the acceptors' step
-    bool la = false;
-    if constexpr (LA) {
-      la = ((kp.cfg & EV_CFG_LA) != 0u) & (ready == 0u) & !pq_old & ((uint32_t)s + 1u < kp.step_cap);
-      use = la ? la_mask & la_allowed() : ready;
-      as = la ? (uint32_t)s + 1u : (uint32_t)s;
-    }
-    const uint32_t s4 = as & 15u;
-    const bool acc = act & (use != 0u);
-    const uint32_t L = acc ? ctz32(use) : 0u;
+    const uint32_t s4 = (uint32_t)s & 15u;
+    const bool acc = act & (ready != 0u);
+    const uint32_t L = acc ? ctz32(ready) : 0u;
     const uint32_t a = L / (uint32_t)PM, p = L - a * (uint32_t)PM;
     const uint32_t wq = m.ld(S::REQ + L);
     const uint32_t kr = S::CMP ? (wq >> S::KSH) : m.ld16(S::RSEQ, L);   // the reply's link sequence number
@@ -741,11 +660,7 @@ struct EvLane {
     // entries, length and reply seq, adjusted in place)
     const uint32_t rq2 = ((wq & ((1u << S::QL) - 1u)) >> 7) + ((wq & ~((1u << S::QL) - 1u)) - (1u << S::QL));
     const bool keep = (len > 1u) & (((wq >> 10) & 15u) == s4);   // the next entry due now too
-    acc_mask = (acc & !la & !keep) ? (acc_mask & ~(1u << L)) : acc_mask;
-    if constexpr (LA) {
-      la_mask = (acc & la & !keep) ? (la_mask & ~(1u << L)) : la_mask;
-      la_any = la_any | (acc & la);
-    }
+    acc_mask = (acc & !keep) ? (acc_mask & ~(1u << L)) : acc_mask;
     in_flight -= acc ? 1u : 0u;
     uint32_t kind, x, z;
     if constexpr (LG) {
@@ -759,7 +674,7 @@ struct EvLane {
     const uint32_t A = get(accw, a);
     const bool dead = ((A >> A_DEAD) & 1u) != 0u;
     const uint32_t wa = get(win, a);                 // isolated at s: c0 <= s < c1 (SEMANTICS §4)
-    const bool isol = ((wa & 0xFFFFu) <= as) & (as < (wa >> 16));
+    const bool isol = ((wa & 0xFFFFu) <= (uint32_t)s) & ((uint32_t)s < (wa >> 16));
     const bool live = acc & !dead & !isol;
     const uint32_t rb = (kind == PROPOSE) ? 12u : 8u;
     canon += acc ? (live ? 2u * rb + 32u : rb) : 0u;
@@ -830,7 +745,6 @@ struct EvLane {
     rp.pw = rx | (ry << 12) | (LG ? 0u : (rz << 24)) | (rk << 30);
     rp.z = rz;
     rp.bit = S::ISH + p * (N + 1) + 1u + a;
-    rp.base = as;
     return w1;
   }
 
@@ -934,8 +848,7 @@ struct EvLane {
   }
   __host__ __device__ __forceinline__ bool end_op(const EvParams& kp, EvOut& o, bool act) {
     if (act && end_ready(kp)) {
-      // (LA: a step that took requests of s + 1 had messages in flight at its end)
-      const bool quiet = (pq_len == 0u) & (in_flight == 0u) & (s >= last_tick) & !(LA & la_any);
+      const bool quiet = (pq_len == 0u) & (in_flight == 0u) & (s >= last_tick);
       // nothing but lost copies at a carried-over step: the instance was quiet at s - 1
       const bool back = EARLY & (canon == canon0);
       // the next step with a due message or a Tick (skews of absent proposers are 0)
@@ -1000,6 +913,30 @@ __host__ inline bool eligible(const pxb_config* c) {
 namespace pxb {
 namespace ev {
 
+// Launch parameters from the ABI config (host side; mirrors pxb_run_device).
+__host__ inline EvParams make_params(const pxb_config* c) {
+  EvParams p{};
+  p.first_instance = c->first_instance;
+  p.k0 = (uint32_t)c->seed;
+  p.k1 = (uint32_t)(c->seed >> 32);
+  p.n_prop = c->n_proposers;
+  p.delay_max = c->delay_max;
+  p.loss_ppm = c->loss_ppm;
+  p.crash_ppm = c->crash_ppm;
+  p.crash_len_max = c->crash_len_max;
+  p.crash_start_max = c->crash_start_max;
+  p.skew_max = c->skew_max;
+  p.step_cap = c->step_cap;
+  p.n_ticks = c->n_ticks > 1 ? c->n_ticks : 1u;
+  p.tick_period = c->n_ticks > 1 ? c->tick_period : 1u;
+  const uint64_t lt = ev_threshold(c->loss_ppm), ct = ev_threshold(c->crash_ppm);
+  p.cfg = ((c->flags & PXB_CFG_RANDOMIZE) ? EV_CFG_RANDOMIZE : 0u) | (lt ? EV_CFG_LOSSY : 0u) | (ct ? EV_CFG_CRASHY : 0u);
+  if ((c->flags & PXB_CFG_RANDOMIZE) || lt || c->delay_max > 1) p.cfg |= EV_CFG_DRAWS;
+  p.loss_m1 = (uint32_t)(lt - 1ull);
+  p.crash_m1 = (uint32_t)(ct - 1ull);
+  return p;
+}
+
 // the timing wheel must outlast the longest delay: sends at step s (or s - 1
 // for a carried-over copy) fall due in [s, s + delay_max] (a link's FIFO tail
 // is at most its last send step + delay_max), the slot of s is emptied on
@@ -1024,41 +961,12 @@ __host__ inline int layout_for(const pxb_config* c) {
   if (c->n_ticks > 1) return 4;                      // log mode: 8-step wheel, 4-entry FIFOs, LG fields
   if (!(c->flags & PXB_CFG_RANDOMIZE) && c->delay_max <= 4 && c->step_cap <= 512 &&
       c->n_proposers * c->n_acceptors <= 16)
-#ifdef PXB_EV_NO_LA
     return 3;
-#else
-    return 2;                                        // (the look-ahead needs the 8-step wheel)
-#endif
   return wheel_for(c->delay_max) == 8 ? 0 : 1;
 }
 __host__ inline int layout_wheel(int layout) { return layout == 1 ? 16 : layout == 3 ? 4 : 8; }
 __host__ inline bool layout_compact(int layout) { return layout == 2 || layout == 3; }
 __host__ inline bool layout_log(int layout) { return layout == 4; }
-
-// Launch parameters from the ABI config (host side; mirrors pxb_run_device).
-__host__ inline EvParams make_params(const pxb_config* c) {
-  EvParams p{};
-  p.first_instance = c->first_instance;
-  p.k0 = (uint32_t)c->seed;
-  p.k1 = (uint32_t)(c->seed >> 32);
-  p.n_prop = c->n_proposers;
-  p.delay_max = c->delay_max;
-  p.loss_ppm = c->loss_ppm;
-  p.crash_ppm = c->crash_ppm;
-  p.crash_len_max = c->crash_len_max;
-  p.crash_start_max = c->crash_start_max;
-  p.skew_max = c->skew_max;
-  p.step_cap = c->step_cap;
-  p.n_ticks = c->n_ticks > 1 ? c->n_ticks : 1u;
-  p.tick_period = c->n_ticks > 1 ? c->tick_period : 1u;
-  const uint64_t lt = ev_threshold(c->loss_ppm), ct = ev_threshold(c->crash_ppm);
-  p.cfg = ((c->flags & PXB_CFG_RANDOMIZE) ? EV_CFG_RANDOMIZE : 0u) | (lt ? EV_CFG_LOSSY : 0u) | (ct ? EV_CFG_CRASHY : 0u);
-  if ((c->flags & PXB_CFG_RANDOMIZE) || lt || c->delay_max > 1) p.cfg |= EV_CFG_DRAWS;
-  p.loss_m1 = (uint32_t)(lt - 1ull);
-  p.crash_m1 = (uint32_t)(ct - 1ull);
-  if (c->delay_max + 2u <= (uint32_t)layout_wheel(layout_for(c))) p.cfg |= EV_CFG_LA;
-  return p;
-}
 
 }  // namespace ev
 }  // namespace pxb

@@ -139,10 +139,6 @@ extern "C" int pxb_trace_instance(const pxb_config* cfg, uint64_t instance, pxb_
                             : pick<false>(cfg->n_proposers, cfg->n_acceptors, wheel_for(cfg->delay_max));
   if (!fn) return PXB_E_INVAL;
   EvParams p = make_params(cfg);
-  // (the production variant runs without the acceptor look-ahead, EvLane::LA:
-  // with it the acceptors may have taken requests of s + 1 when step s is
-  // recorded; the batch-kernel parity tests cover the look-ahead)
-  p.cfg &= ~EV_CFG_LA;
   p.first_instance = instance;
   pxb_trace_step* d_out = nullptr;
   uint32_t* d_st = nullptr;

@@ -224,4 +224,4 @@ def test_random_log_mode_schedules(i):
         step_cap=int(rng.choice([int(rng.integers(1, 64)), 512, 2048])),
         n_ticks=int(rng.integers(2, 60)), tick_period=int(rng.integers(1, 16)),
         randomize=bool(rng.random() < 0.3))
-    check(cfg, int(rng.integers(0, 1 << 34)), int(rng.integers(1, 500)), max_bail_frac=0.6)   # (P = 3, N = 9 with 25 Ticks: about half bail)
+    check(cfg, int(rng.integers(0, 1 << 34)), int(rng.integers(1, 500)), max_bail_frac=0.5)

@@ -17,6 +17,6 @@ for k, v in j.get("extra", {}).items():
         print("%s %.2f M/s%s" % (k, v["instances_per_s"] / 1e6, (" (x%.2f vs general kernel)" % v["speedup_vs_general_kernel"]) if "speedup_vs_general_kernel" in v else ""))
 PY
 if [ $# -gt 0 ]; then
-  AB_CASES=${AB_CASES:-4:8388608:1,3:4194304:2,7:1048576:2} timeout -k 10 400 python3 -u tools/ab_ev.py "$@" "$@" > gpurun_out/r3b/ab.txt 2>&1 || { cat gpurun_out/r3b/ab.txt; exit 1; }
+  AB_CASES=4:8388608:1,3:4194304:2 timeout -k 10 400 python3 -u tools/ab_ev.py "$@" "$@" > gpurun_out/r3b/ab.txt 2>&1 || { cat gpurun_out/r3b/ab.txt; exit 1; }
   cat gpurun_out/r3b/ab.txt
 fi
