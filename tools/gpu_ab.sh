@@ -1,8 +1,9 @@
 #!/bin/bash
-# A/B the variant libraries given as arguments (tools/ab_ev.py), twice each, interleaved.
+# A/B of per-lane-kernel library variants (tools/ab_ev.py), two passes:
+#   bash tools/gpu_ab.sh lib1.so lib2.so ...   (AB_CASES as in ab_ev.py)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R && mkdir -p gpurun_out/ab
 for l in "$@"; do test -f "$l" || { echo "missing $l"; exit 1; }; done
-timeout -k 10 600 python3 -u tools/ab_ev.py "$@" "$@" > gpurun_out/ab/ab.txt 2>&1; rc=$?
-cat gpurun_out/ab/ab.txt; exit $rc
+AB_CASES=${AB_CASES:-4:8388608:1,3:4194304:2} timeout -k 10 600 python3 -u tools/ab_ev.py "$@" "$@" > gpurun_out/ab/ab.txt 2>&1 || { cat gpurun_out/ab/ab.txt; exit 1; }
+cat gpurun_out/ab/ab.txt
