@@ -219,7 +219,6 @@ struct EvLane {
   bool pq_old;                        // the head pending broadcast was made at step s - 1
   uint32_t canon0;                    // canon on entering a step that carries one over (else canon - 1)
   pool_mask_t pfree;                  // free response-pool words
-  uint32_t in_flight;
   uint32_t lflags, rounds, dval, dtick, execs, msgs, canon;
   unsigned long long clog;            // canonical log, 2-bit values (divergence check, SEMANTICS §7)
   uint32_t clog_len;
@@ -239,6 +238,13 @@ struct EvLane {
     __asm__("" : "+v"(x));
 #endif
     return x;
+  }
+  // keeps a rarely taken branch a branch: SimplifyCFG's speculation would
+  // otherwise run its body as selects in every iteration
+  __host__ __device__ static __forceinline__ void opaque_barrier() {
+#if defined(__HIP_DEVICE_COMPILE__)
+    __asm__ volatile("");
+#endif
   }
   // Selects by a per-lane index q over a small register array, as bit
   // operations on the one-hot word 1 << q: element i's lane mask is bit i of
@@ -353,6 +359,7 @@ struct EvLane {
     // Ticks only up to the last skew
     uint32_t tk = 0u;
     if (any_lane(t <= last_tick)) {                 // (single decree: the first steps only)
+      opaque_barrier();
       tk = (t <= last_tick) ? ticks_at(t) : 0u;
       if constexpr (LG) {                            // the next Tick of each proposer that ticked
 #pragma unroll
@@ -443,7 +450,6 @@ struct EvLane {
     pq = pq_len = acur = 0u;
     pq_old = false;
     pfree = full_pool();
-    in_flight = 0u;
     lflags = rounds = dval = dtick = execs = msgs = canon = 0u;
     clog = 0ull;
     clog_len = 0u;
@@ -482,8 +488,12 @@ struct EvLane {
       }
     }
     pq |= (p0 ? ((q << 3) | slot0) << (5u * pq_len) : 0u) | (p1 ? ((q << 3) | slot1) << (5u * pq_len + 5u) : 0u);
-    pq_len += (p0 ? 1u : 0u) + (p1 ? 1u : 0u);
-    put(bnext, q, (slot0 + (p0 ? 1u : 0u) + (p1 ? 1u : 0u)) & (S::BR - 1u));
+    const uint32_t nb = (p0 ? 1u : 0u) + (p1 ? 1u : 0u);
+    pq_len += nb;
+    // every copy is counted here: an instance ends (quiet or at the step cap)
+    // only with no broadcast left to send (end_op)
+    msgs += nb * (uint32_t)N;
+    put(bnext, q, (slot0 + nb) & (S::BR - 1u));
   }
 
   // the next copy of the oldest pending broadcast, on link cp -> ca (Philox
@@ -517,7 +527,6 @@ struct EvLane {
       pq_old = pq_old & !wrap;
       put(nsent, cp, ck + (wrap ? 1u : 0u));
     }
-    msgs += csnd ? 1u : 0u;                          // (the reply counted itself)
     const bool snd = isR | csnd;
     const bool ok = !(lossy & (w.x <= loss_m1));
     const uint32_t d = 1u + mulhi_n(w.y, dmax);
@@ -557,7 +566,6 @@ struct EvLane {
     m.orw(S::WHEEL + slot * S::WW + ((S::WW == 2 && isR) ? 1u : 0u), (go & !now) ? 1u << (isR ? rp.bit : Lq) : 0u);
     occ |= (go & !now) ? (1u << slot) : 0u;
     acc_mask |= (go & now) ? (1u << Lq) : 0u;
-    in_flight += go ? 1u : 0u;
   }
 
   // the Philox counter words of the next copy (seq = the broadcast's index on
@@ -586,7 +594,6 @@ struct EvLane {
     // (w: the draw of copy_ctr() taken before this call)
     const bool ok = !(lossy & (w.x <= loss_m1));
     const uint32_t d = 1u + mulhi_n(w.y, dmax);      // (delay_max <= 1: always 1)
-    msgs += snd ? 1u : 0u;
     // enqueue (predicated: inactive lanes store to the dummy word)
     const bool go = snd & ok;
     const uint32_t Lq = ca * (uint32_t)PM + cp;
@@ -607,7 +614,6 @@ struct EvLane {
     m.orw(S::WHEEL + slot * S::WW, (go & !now) ? 1u << Lq : 0u);
     occ |= (go & !now) ? (1u << slot) : 0u;
     acc_mask |= (go & now) ? (1u << Lq) : 0u;
-    in_flight += go ? 1u : 0u;
   }
 
   // One iteration: the proposer part, a copy, the acceptor part, another
@@ -661,7 +667,6 @@ struct EvLane {
     const uint32_t rq2 = ((wq & ((1u << S::QL) - 1u)) >> 7) + ((wq & ~((1u << S::QL) - 1u)) - (1u << S::QL));
     const bool keep = (len > 1u) & (((wq >> 10) & 15u) == s4);   // the next entry due now too
     acc_mask = (acc & !keep) ? (acc_mask & ~(1u << L)) : acc_mask;
-    in_flight -= acc ? 1u : 0u;
     uint32_t kind, x, z;
     if constexpr (LG) {
       const uint32_t w32 = m.ld(S::BRING + p * S::BR + bslot);
@@ -774,7 +779,6 @@ struct EvLane {
       const bool nnow = nkc ? ((nk & 7u) == (s4 & 7u)) : (((pn >> 26) & 15u) == s4);
       const bool rkeep = resp & (rlen > 1u) & nnow;
       in_mask = (pin & !rkeep) ? (in_mask & ~(1u << j)) : in_mask;
-      in_flight -= resp ? 1u : 0u;
       const uint32_t rkind = pe >> 30, px = pe & 0xFFFu, py = (pe >> 12) & 0xFFFu;
       const uint32_t pz = LG ? m.ld16h(S::POOLZ + (k >> 1), k & 1u) : (pe >> 24) & 3u;
       canon += resp ? 2u * (16u >> rkind) : 0u;         // Round1OK 16, HaveTicket 8, Round2Success 4
@@ -848,16 +852,20 @@ struct EvLane {
   }
   __host__ __device__ __forceinline__ bool end_op(const EvParams& kp, EvOut& o, bool act) {
     if (act && end_ready(kp)) {
-      const bool quiet = (pq_len == 0u) & (in_flight == 0u) & (s >= last_tick);
+      // (no message in flight: every queued one falls due after s and holds a
+      // bit of its due step's wheel slot, which only entering that step clears)
+      const bool quiet = (pq_len == 0u) & (occ == 0u) & (s >= last_tick);
       // nothing but lost copies at a carried-over step: the instance was quiet at s - 1
       const bool back = EARLY & (canon == canon0);
       // the next step with a due message or a Tick (skews of absent proposers are 0)
       const uint32_t s1 = (uint32_t)s + 1u;
       const uint32_t rot = ((occ >> (s1 & WM)) | (occ << ((W - (s1 & WM)) & WM))) & ((1u << W) - 1u);
       uint32_t nx = ((occ != 0u) & (pq_len == 0u)) ? s1 + ctz32(rot) : (pq_len ? s1 : 0xFFFFu);
-      if (any_lane(s < last_tick))                    // (a later Tick: first steps only)
+      if (any_lane(s < last_tick)) {                  // (a later Tick: first steps only)
+        opaque_barrier();
 #pragma unroll
-      for (int q = 0; q < PM; ++q) nx = ((skew[q] > (uint32_t)s) & (skew[q] < nx)) ? skew[q] : nx;
+        for (int q = 0; q < PM; ++q) nx = ((skew[q] > (uint32_t)s) & (skew[q] < nx)) ? skew[q] : nx;
+      }
       const bool capped = !quiet & (nx >= kp.step_cap);
       if (__builtin_expect(quiet | capped, 0)) {
         s = capped ? (int32_t)kp.step_cap - 1 : (back ? s - 1 : s);
@@ -884,6 +892,13 @@ struct EvLane {
     o.flags = f;
     o.steps = steps;
     mode = M_IDLE;
+  }
+
+  // messages queued on the links (the trace's in_flight; the kernels test the wheel)
+  __host__ __device__ uint32_t links_in_flight() const {
+    uint32_t n = 0u;
+    for (uint32_t L = 0; L < NLQ; ++L) n += ((m.ld(S::REQ + L) >> S::QL) & QLM) + ((m.ld(S::RSP + L) >> S::RL) & RLM);
+    return n;
   }
 
   // final per-acceptor outputs (digest, record) of an ended instance

@@ -16,7 +16,7 @@ __device__ void trace_record(const EvLane<PM, N, POOL, W, false, Mem, EARLY>& L,
   r->step = step;
   // (production variant: copies of a broadcast still to send are not on the
   // links yet, so the count is not the oracle's end-of-step one)
-  r->in_flight = (EARLY && L.pq_len != 0u) ? PXB_TRACE_IN_FLIGHT_UNKNOWN : L.in_flight;
+  r->in_flight = (EARLY && L.pq_len != 0u) ? PXB_TRACE_IN_FLIGHT_UNKNOWN : L.links_in_flight();
   r->n_acceptors = N;
   r->n_proposers = L.P;
   for (int a = 0; a < PXB_MAX_ACCEPTORS; ++a) {
