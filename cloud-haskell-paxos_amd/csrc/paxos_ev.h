@@ -97,8 +97,9 @@ struct Shape {
   static constexpr int POOLW = RSP + NLQ;            // POOL response words
   // broadcast ring slots per proposer: short-delay (compact) schedules never
   // hold more than 4 broadcasts of one proposer in flight (BASELINE configs
-  // 3 and 4: the bail rate is the same with 4 slots as with 8)
-  static constexpr uint32_t BR = CMP ? 4 : 8;
+  // 3 and 4: the bail rate is the same with 4 slots as with 8), nor does
+  // faulty log mode (extra.log_mode_faulty: no bail with 4)
+  static constexpr uint32_t BR = (CMP || LG) ? 4 : 8;
   // log mode: the responses' 14-bit commands in a halfword array beside the
   // pool (+ one dummy halfword), the first LOG_TRACK positions of the
   // canonical log (halfwords), 32-bit broadcast payloads
@@ -126,7 +127,9 @@ struct Shape {
 //   acceptor word       t_max [11:0] | t_store [23:12] | val [25:24] | dead [26] | log_len [31:27]
 //   window              c0 [15:0] | c1 [31:16]  (clamped to 4096: steps are < 4095)
 // Log mode (LG) carries commands "c<id>.<t>" as 14 bits, id [13:12] | t [11:0]
-// (t >= 1; 0 = Nothing), so:
+// (t >= 1; 0 = Nothing) and keeps 4 broadcast ring slots per proposer (with
+// the 18-word response pool of topologies of <= 10 links, EvPool: 85 words per
+// lane for P = 2, N = 5, 7 waves per CU), so:
 //   acceptor word       t_max [11:0] | t_store [23:12] | dead [24]; a second word (accv):
 //                       the stored command [13:0] | log_len [31:14]
 //   response word       z [25:24] unused: the command in the pool's halfword array

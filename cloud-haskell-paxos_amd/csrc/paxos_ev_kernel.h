@@ -66,9 +66,16 @@ struct EvKParams {
 #ifndef PXB_EV_CMP_POOL
 #define PXB_EV_CMP_POOL 24
 #endif
-template <int PM, int N, bool CMP>
+// (log mode over at most 10 links: 18 words, which faulty log mode's batch never
+// fills (extra.log_mode_faulty: no bail in 20000 instances): 85 words per lane,
+// 7 waves per CU instead of 5)
+template <int PM, int N, bool CMP, bool LG = false>
 struct EvPool {
-  static constexpr int value = (PM * N <= 16) ? (CMP ? PXB_EV_CMP_POOL : 32) : CMP ? 48 : (PM * N <= 18) ? 32 : 64;
+  static constexpr int value = (LG && PM * N <= 10) ? 18
+                               : (PM * N <= 16)     ? (CMP ? PXB_EV_CMP_POOL : 32)
+                               : CMP                ? 48
+                               : (PM * N <= 18)     ? 32
+                                                    : 64;
 };
 
 // Run totals: each lane sums its finished instances in registers; the wave
@@ -116,7 +123,7 @@ struct EvTotals {
 // bound (minimum waves per SIMD) makes the compiler keep to.
 template <int PM, int N, int W, bool CMP, bool LG = false>
 __global__ __launch_bounds__(64, CMP ? 3 : 1) void paxos_ev_kernel(EvKParams kp) {
-  constexpr int POOL = EvPool<PM, N, CMP>::value;
+  constexpr int POOL = EvPool<PM, N, CMP, LG>::value;
   using S = Shape<PM, N, POOL, W, CMP, LG>;
   __shared__ uint32_t lds[S::WORDS * 64];
   const uint32_t lane = threadIdx.x;

@@ -30,7 +30,7 @@ struct HostMem {
 template <int PM, int N, int W, bool CMP, bool LG>
 int run_shape(const pxb_config* cfg, pxb_result* out, uint32_t* dig, pxb_acceptor_rec* acc, int64_t* tot,
               uint32_t* bail_ids, uint32_t* n_bail, uint64_t* micro_steps) {
-  constexpr int POOL = EvPool<PM, N, CMP>::value;
+  constexpr int POOL = EvPool<PM, N, CMP, LG>::value;
   using S = Shape<PM, N, POOL, W, CMP, LG>;
   std::vector<uint32_t> buf(S::WORDS + 1, 0xDEADBEEFu);   // garbage: init must set what it reads
   const EvParams p = make_params(cfg);
