@@ -66,11 +66,12 @@ static_assert(MAX_STEP_CAP < PXB_TICKET_LIMIT, "EV tickets never reach the overf
 // lane modes
 constexpr uint32_t M_IDLE = 0, M_RUN = 1;
 
-template <int PM_, int N_, int POOL_, int W_, bool CMP_, bool LG_ = false>
+template <int PM_, int N_, int POOL_, int W_, bool CMP_, bool LG_ = false, bool SL_ = false>
 struct Shape {
   static constexpr int PM = PM_, N = N_, POOL = POOL_, W = W_;
   static constexpr bool CMP = CMP_;                  // compact links (see Layouts)
   static constexpr bool LG = LG_;                    // log mode (several Ticks, long logs; see Layouts)
+  static constexpr bool SL = SL_;                    // slim 4-entry layout (see Layouts)
   static constexpr int NLQ = PM * N;                 // request (and response) links
   static constexpr int NIN = PM * (N + 1);           // proposer-input bits (Tick + N links each)
   static constexpr int WW = (NLQ + NIN <= 32) ? 1 : 2;   // wheel words per slot
@@ -93,13 +94,14 @@ struct Shape {
   // LDS word offsets
   static constexpr int REQ = 0;                      // NLQ: request links, index a*PM + p (CMP: + reply seq)
   static constexpr int RSEQ = REQ + NLQ;             // !CMP: NLQ halfwords of reply seq, index a*PM + p
-  static constexpr int RSP = RSEQ + (CMP ? 0 : (NLQ + 1) / 2);   // NLQ response links, index p*N + a
+  // (slim: the reply seqs are bytes in registers)
+  static constexpr int RSP = RSEQ + ((CMP || SL) ? 0 : (NLQ + 1) / 2);   // NLQ response links, index p*N + a
   static constexpr int POOLW = RSP + NLQ;            // POOL response words
   // broadcast ring slots per proposer: short-delay (compact) schedules never
   // hold more than 4 broadcasts of one proposer in flight (BASELINE configs
   // 3 and 4: the bail rate is the same with 4 slots as with 8), nor does
   // faulty log mode (extra.log_mode_faulty: no bail with 4)
-  static constexpr uint32_t BR = (CMP || LG) ? 4 : 8;
+  static constexpr uint32_t BR = (CMP || LG || SL) ? 4 : 8;
   // log mode: the responses' 14-bit commands in a halfword array beside the
   // pool (+ one dummy halfword), the first LOG_TRACK positions of the
   // canonical log (halfwords), 32-bit broadcast payloads
@@ -126,6 +128,11 @@ struct Shape {
 //   broadcast payload   x [11:0] | z [13:12] | kind [15:14]
 //   acceptor word       t_max [11:0] | t_store [23:12] | val [25:24] | dead [26] | log_len [31:27]
 //   window              c0 [15:0] | c1 [31:16]  (clamped to 4096: steps are < 4095)
+// Slim (SL, layout 5: the 4-entry layout on the 8-step wheel for runs of at
+// most 512 steps, BASELINE config 5): the reply seqs are bytes in registers
+// (a 256th reply on one link bails), 4 broadcast ring slots per proposer, and
+// the response pools of EvPool: 120 LDS words per lane for P = 3, N = 9 (5
+// waves per CU instead of 4), 86 for P = 2 (7 instead of 6).
 // Log mode (LG) carries commands "c<id>.<t>" as 14 bits, id [13:12] | t [11:0]
 // (t >= 1; 0 = Nothing) and keeps 4 broadcast ring slots per proposer (with
 // the 18-word response pool of topologies of <= 10 links, EvPool: 85 words per
@@ -180,9 +187,9 @@ struct EvOut {
 // EARLY: a step may end with the copies of its last broadcast still to send
 // (see end_op); the trace kernel turns it off so that its per-step records
 // hold every message of the step in flight, as the oracle's do.
-template <int PM, int N, int POOL, int W, bool CMP, class Mem, bool EARLY = true, bool LG = false>
+template <int PM, int N, int POOL, int W, bool CMP, class Mem, bool EARLY = true, bool LG = false, bool SL = false>
 struct EvLane {
-  using S = Shape<PM, N, POOL, W, CMP, LG>;
+  using S = Shape<PM, N, POOL, W, CMP, LG, SL>;
   // acceptor fields (Layouts): dead bit, log-length shift (LG: in accv) and its limit
   static constexpr uint32_t A_DEAD = LG ? 24 : 26, A_LEN = LG ? 14 : 27, A_LEN_MAX = LG ? (1u << 18) - 1u : 31;
   using pool_mask_t = typename std::conditional<(POOL > 32), unsigned long long, uint32_t>::type;
@@ -218,6 +225,7 @@ struct EvLane {
   // acceptor states (Server.hs:24-31), isolation windows, log digests
   uint32_t accw[N], win[N], accd[N];
   uint32_t accv[LG ? N : 1];          // LG: the stored command and log length of each acceptor
+  uint32_t rseqv[SL ? (NLQ + 3) / 4 : 1];   // SL: the reply seqs, a byte per request link
   uint32_t pq, pq_len, acur;          // pending broadcasts (p << 3 | slot, 5 bits each), next acceptor
   bool pq_old;                        // the head pending broadcast was made at step s - 1
   uint32_t canon0;                    // canon on entering a step that carries one over (else canon - 1)
@@ -448,6 +456,10 @@ struct EvLane {
     }
 #pragma unroll
     for (int i = S::REQ; i < S::POOLW; ++i) m.st(i, 0u);     // request links, reply seqs, response links
+    if constexpr (SL) {
+#pragma unroll
+      for (int i = 0; i < (int)((NLQ + 3) / 4); ++i) rseqv[i] = 0u;
+    }
 #pragma unroll
     for (int i = 0; i < W * S::WW; ++i) m.st(S::WHEEL + i, 0u);
     pq = pq_len = acur = 0u;
@@ -662,7 +674,9 @@ struct EvLane {
     const uint32_t L = acc ? ctz32(ready) : 0u;
     const uint32_t a = L / (uint32_t)PM, p = L - a * (uint32_t)PM;
     const uint32_t wq = m.ld(S::REQ + L);
-    const uint32_t kr = S::CMP ? (wq >> S::KSH) : m.ld16(S::RSEQ, L);   // the reply's link sequence number
+    // the reply's link sequence number
+    const uint32_t kw = SL ? get(rseqv, L >> 2) : 0u;
+    const uint32_t kr = S::CMP ? (wq >> S::KSH) : SL ? (kw >> (8u * (L & 3u))) & 0xFFu : m.ld16(S::RSEQ, L);
     const uint32_t len = (wq >> S::QL) & QLM;
     const uint32_t bslot = wq & 7u;
     // the popped word: entries shifted down one, length - 1 (fields above the
@@ -746,8 +760,9 @@ struct EvLane {
     // (one draw: this reply's, or, without one, the next copy's: cc)
     const uint4 w1 = draw(snd1 ? kr : cc.x, snd1 ? (1u << 24) | (1u << 16) | (p << 8) | a : cc.y);
     msgs += snd1 ? 1u : 0u;
-    bailed = bailed | (snd1 & (kr == (S::CMP ? (1u << S::KB) - 1u : 0xFFFFu)));
-    if (!S::CMP) m.st16(S::RSEQ, L, snd1 ? kr + 1u : kr);
+    bailed = bailed | (snd1 & (kr == (S::CMP ? (1u << S::KB) - 1u : SL ? 0xFFu : 0xFFFFu)));
+    if constexpr (SL) put(rseqv, L >> 2, kw + (snd1 ? 1u << (8u * (L & 3u)) : 0u));
+    else if constexpr (!S::CMP) m.st16(S::RSEQ, L, snd1 ? kr + 1u : kr);
     rp.snd = snd1;
     rp.Lr = p * (uint32_t)N + a;
     rp.pw = rx | (ry << 12) | (LG ? 0u : (rz << 24)) | (rk << 30);
@@ -974,13 +989,18 @@ __host__ inline int wheel_for(uint32_t delay_max) { return delay_max <= 8 ? 8 : 
 // over 9 acceptors overflow the 3-entry FIFOs too often (25 % of instances at
 // 10 % loss), so the compact layout is kept to topologies of <= 16 links.
 // Layout 3 is the compact layout with a 4-step wheel (delays up to 4: BASELINE
-// configs 3 and 4), 4 words per lane fewer.
+// configs 3 and 4), 4 words per lane fewer.  Layout 5 is layout 0 slimmed
+// (Shape::SL) for runs of at most 512 steps (BASELINE config 5).
 __host__ inline int layout_for(const pxb_config* c) {
   if (c->n_ticks > 1) return 4;                      // log mode: 8-step wheel, 4-entry FIFOs, LG fields
   if (!(c->flags & PXB_CFG_RANDOMIZE) && c->delay_max <= 4 && c->step_cap <= 512 &&
       c->n_proposers * c->n_acceptors <= 16)
     return 3;
-  return wheel_for(c->delay_max) == 8 ? 0 : 1;
+  if (wheel_for(c->delay_max) != 8) return 1;
+#ifndef PXB_EV_NO_SLIM
+  if (c->step_cap <= 512) return 5;                  // slim: byte reply seqs suffice
+#endif
+  return 0;
 }
 __host__ inline int layout_wheel(int layout) { return layout == 1 ? 16 : layout == 3 ? 4 : 8; }
 __host__ inline bool layout_compact(int layout) { return layout == 2 || layout == 3; }

@@ -1,8 +1,8 @@
 // paxos_ev.hip — explicit instantiations of the per-lane kernel
 // (paxos_ev_kernel.h) for one proposer count (-DPXB_EV_P=1|2|3): 8 acceptor
 // counts x {8, 16}-step timing wheels (plus the compact-link
-// layout with the 8- and 4-step wheels, and the log-mode fields on the 8-step
-// wheel).  Split by P so the units build in
+// layout with the 8- and 4-step wheels, the log-mode fields on the 8-step
+// wheel, and the slim 8-step layout).  Split by P so the units build in
 // parallel.
 #include "paxos_ev_kernel.h"
 
@@ -12,13 +12,15 @@
 
 namespace pxb {
 namespace ev {
-#define PXB_EV_INST(N, W, C, L) template __global__ void paxos_ev_kernel<PXB_EV_P, N, W, C, L>(EvKParams);
-#define PXB_EV_FOR_N(W, C, L) PXB_EV_INST(2, W, C, L) PXB_EV_INST(3, W, C, L) PXB_EV_INST(4, W, C, L) \
-  PXB_EV_INST(5, W, C, L) PXB_EV_INST(6, W, C, L) PXB_EV_INST(7, W, C, L) PXB_EV_INST(8, W, C, L) PXB_EV_INST(9, W, C, L)
-PXB_EV_FOR_N(8, false, false)
-PXB_EV_FOR_N(16, false, false)
-PXB_EV_FOR_N(8, true, false)
-PXB_EV_FOR_N(4, true, false)
-PXB_EV_FOR_N(8, false, true)     // log mode
+#define PXB_EV_INST(N, W, C, L, S) template __global__ void paxos_ev_kernel<PXB_EV_P, N, W, C, L, S>(EvKParams);
+#define PXB_EV_FOR_N(W, C, L, S) PXB_EV_INST(2, W, C, L, S) PXB_EV_INST(3, W, C, L, S) PXB_EV_INST(4, W, C, L, S) \
+  PXB_EV_INST(5, W, C, L, S) PXB_EV_INST(6, W, C, L, S) PXB_EV_INST(7, W, C, L, S) PXB_EV_INST(8, W, C, L, S) \
+  PXB_EV_INST(9, W, C, L, S)
+PXB_EV_FOR_N(8, false, false, false)
+PXB_EV_FOR_N(16, false, false, false)
+PXB_EV_FOR_N(8, true, false, false)
+PXB_EV_FOR_N(4, true, false, false)
+PXB_EV_FOR_N(8, false, true, false)     // log mode
+PXB_EV_FOR_N(8, false, false, true)     // slim
 }  // namespace ev
 }  // namespace pxb

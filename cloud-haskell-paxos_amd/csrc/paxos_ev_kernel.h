@@ -69,12 +69,15 @@ struct EvKParams {
 // (log mode over at most 10 links: 18 words, which faulty log mode's batch never
 // fills (extra.log_mode_faulty: no bail in 20000 instances): 85 words per lane,
 // 7 waves per CU instead of 5)
-template <int PM, int N, bool CMP, bool LG = false>
+// (slim: 44 words hold the responses of 98.4 % of config 5's P = 3 instances,
+// 30 those of 99.99 % of its P = 2 ones)
+template <int PM, int N, bool CMP, bool LG = false, bool SL = false>
 struct EvPool {
   static constexpr int value = (LG && PM * N <= 10) ? 18
                                : (PM * N <= 16)     ? (CMP ? PXB_EV_CMP_POOL : 32)
                                : CMP                ? 48
-                               : (PM * N <= 18)     ? 32
+                               : (PM * N <= 18)     ? (SL ? 30 : 32)
+                               : SL                 ? 44
                                                     : 64;
 };
 
@@ -121,16 +124,17 @@ struct EvTotals {
 // The compact layout leaves room for 10 resident waves per CU (LDS), i.e. 3
 // on some SIMDs: its register budget is then 168 VGPRs, which the second
 // bound (minimum waves per SIMD) makes the compiler keep to.
-template <int PM, int N, int W, bool CMP, bool LG = false>
-__global__ __launch_bounds__(64, CMP ? 3 : 1) void paxos_ev_kernel(EvKParams kp) {
-  constexpr int POOL = EvPool<PM, N, CMP, LG>::value;
-  using S = Shape<PM, N, POOL, W, CMP, LG>;
+// The slim layout fits 5 or more waves per CU, 2 on some SIMDs: <= 256 VGPRs.
+template <int PM, int N, int W, bool CMP, bool LG = false, bool SL = false>
+__global__ __launch_bounds__(64, CMP ? 3 : SL ? 2 : 1) void paxos_ev_kernel(EvKParams kp) {
+  constexpr int POOL = EvPool<PM, N, CMP, LG, SL>::value;
+  using S = Shape<PM, N, POOL, W, CMP, LG, SL>;
   __shared__ uint32_t lds[S::WORDS * 64];
   const uint32_t lane = threadIdx.x;
   unsigned long long* const trow = kp.part + (size_t)(blockIdx.x % EV_TCOPIES) * 16u;
   EvTotals tot;
   tot.clear();
-  EvLane<PM, N, POOL, W, CMP, LdsMem, true, LG> L;
+  EvLane<PM, N, POOL, W, CMP, LdsMem, true, LG, SL> L;
   L.m = LdsMem{lds, lane};
   L.set_keys(kp.p);
   L.mode = M_IDLE;

@@ -124,16 +124,29 @@ def test_random_schedules(i):
     check(cfg, int(rng.integers(0, 1 << 34)), int(rng.integers(1, 800)), max_bail_frac=0.5)
 
 
-@pytest.mark.parametrize("layout", [0, 2, 3])
+@pytest.mark.parametrize("layout", [0, 2, 3, 5])
 @pytest.mark.parametrize("c", [3, 4])
 def test_layouts(c, layout, monkeypatch):
     """Every link layout (4-entry FIFOs; the compact 3-entry FIFOs with the
     reply seq packed beside the request FIFO, on the 8- and on the 4-step
-    timing wheel) on the short-delay configs."""
+    timing wheel; the slim 4-entry layout with byte reply seqs in registers)
+    on the short-delay configs."""
     monkeypatch.setenv("EV_LAYOUT", str(layout))
     _, _, bails = check(pxb.CONFIGS[c], 5000, 2000, max_bail_frac=0.03)
-    if layout == 0:
+    if layout in (0, 5):
         assert len(bails) == 0
+
+
+@pytest.mark.parametrize("layout", [0, 5])
+@pytest.mark.parametrize("pm", [2, 3])
+def test_config5_8step_layouts(pm, layout, monkeypatch):
+    """Config 5 (fuzzed P <= 3, delays to 8) on both 8-step-wheel layouts and
+    both shapes of the split routing (EV_PM: the shape's proposer capacity;
+    instances that drew more bail at init): the slim layout (byte reply seqs,
+    4 ring slots, 44- / 30-word pools) bails about as rarely as the full one."""
+    monkeypatch.setenv("EV_LAYOUT", str(layout))
+    monkeypatch.setenv("EV_PM", str(pm))
+    check(pxb.CONFIGS[5], 3000, 1500, max_bail_frac=0.75 if pm == 2 else 0.03)
 
 
 @pytest.mark.parametrize("layout", [2, 3])
