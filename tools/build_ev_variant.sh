@@ -3,7 +3,8 @@
 # Rebuilds only the per-lane kernel units (paxos_ev_p1..3, trace) with the
 # extra flags and links them with the current build's other objects: A/B of
 # paxos_ev.h changes in a minute instead of a full library build.  EVP1 / EVP2
-# / EVP3 in the environment add flags to one proposer count's unit only.
+# / EVP3 in the environment add flags to one proposer count's unit only;
+# EV_FLAGS_OVERRIDE replaces __graft_entry__.EV_FLAGS for the variant.
 set -e
 R=$(cd $(dirname $0)/.. && pwd)
 mkdir -p $R/variants
@@ -15,6 +16,8 @@ import __graft_entry__ as g
 g._hip_objects()                       # the base objects, up to date
 tag = '_' + sys.argv[1]
 extra = sys.argv[2:]
+if os.environ.get('EV_FLAGS_OVERRIDE') is not None:   # replace the per-lane units' LLVM flags
+    g.EV_FLAGS = os.environ['EV_FLAGS_OVERRIDE'].split()
 procs, objs = [], []
 for p in (1, 2, 3):
     o = os.path.join(g.OBJ_DIR, 'paxos_ev_p%d%s.o' % (p, tag))
