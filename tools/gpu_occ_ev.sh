@@ -1,5 +1,5 @@
 #!/bin/bash
-# Residency sweep of the per-lane kernel: config 4 (and 3) with the launch
+# Residency sweep of the per-lane kernel: config 4 (and 3; OCC_KS, OCC_CS choose) with the launch
 # capped at K blocks (= waves) per CU (PXB_BLOCKS_PER_CU).   bash tools/gpu_occ_ev.sh [lib]
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
