@@ -16,6 +16,8 @@ using namespace pxb::ev;
 
 namespace {
 
+int g_words = 0;                                           // LDS words per lane of the last shape run
+
 struct HostMem {
   uint32_t* w;
   uint32_t ld(uint32_t i) const { return w[i]; }
@@ -32,6 +34,7 @@ int run_shape(const pxb_config* cfg, pxb_result* out, uint32_t* dig, pxb_accepto
               uint32_t* bail_ids, uint32_t* n_bail, uint64_t* micro_steps) {
   constexpr int POOL = EvPool<PM, N, CMP, LG, SL>::value;
   using S = Shape<PM, N, POOL, W, CMP, LG, SL>;
+  g_words = S::WORDS;
   std::vector<uint32_t> buf(S::WORDS + 1, 0xDEADBEEFu);   // garbage: init must set what it reads
   const EvParams p = make_params(cfg);
   EvLane<PM, N, POOL, W, CMP, HostMem, true, LG, SL> L;
@@ -145,3 +148,6 @@ extern "C" int ev_host_run(const pxb_config* cfg, pxb_result* out, uint32_t* dig
   }
   return -1;
 }
+
+// the LDS words per lane of the shape the last ev_host_run used (tests: layout sizes)
+extern "C" int ev_host_last_words(void) { return g_words; }

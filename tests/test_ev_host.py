@@ -238,3 +238,24 @@ def test_random_log_mode_schedules(i):
         n_ticks=int(rng.integers(2, 60)), tick_period=int(rng.integers(1, 16)),
         randomize=bool(rng.random() < 0.3))
     check(cfg, int(rng.integers(0, 1 << 34)), int(rng.integers(1, 500)), max_bail_frac=0.5)
+
+
+# LDS per lane of the shapes the bench workloads run, and the residency it buys.
+# A 64-lane block of W words takes 256 W bytes of the CU's 160 KiB; blocks that
+# fill it to within ~1 KiB measured no gain ("LDS to spare"), so
+# every shape keeps >= 7 KiB free at its residency.
+@pytest.mark.parametrize("c,pm,words,blocks", [
+    (4, 2, 60, 10),      # compact, 4-step wheel
+    (3, 2, 44, 12),      # compact, 16-word pool (12 = the VGPR limit)
+    (5, 3, 120, 5),      # slim, P = 3 share
+    (5, 2, 86, 7),       # slim, P <= 2 share
+    (7, 2, 85, 7),       # faulty log mode
+])
+def test_layout_words_leave_lds_to_spare(c, pm, words, blocks, monkeypatch):
+    cfg = pxb.CONFIGS[c]
+    if pm != cfg.n_proposers:
+        monkeypatch.setenv("EV_PM", str(pm))
+    ev_run(cfg, 0, 1)
+    assert lib().ev_host_last_words() == words
+    assert blocks * 256 * words <= 160 * 1024 - 7 * 1024
+
