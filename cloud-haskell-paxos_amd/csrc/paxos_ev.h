@@ -81,8 +81,16 @@ struct Shape {
   // reply seq of the same (a, p) pair in the word's top KB bits
   static constexpr int QC = CMP ? 3 : 4, QL = 7 * QC, QLB = CMP ? 2 : 3;
   static constexpr int KSH = QL + QLB, KB = 32 - KSH;
-  // response FIFO: RC pool indices of IB bits, length at RL (RLB bits), tail due at RD
-  static constexpr int RC = 4, RL = IB * RC, RLB = 3, RD = RL + RLB;
+  // response FIFO: RC pool indices of IB bits, length at RL (RLB bits), tail due at RD;
+  // slim over > 18 links (RSN): RC = 5 entries, each its pool index + 1 (0: empty),
+  // no length or due field (the length from the highest set bit, the tail's due
+  // from its pool word).  Config 5's three-proposer shape: P = 3 bails 1.7 % ->
+  // 0.4 % of instances, the general kernel 53 -> 17 ms at 2^25, the per-lane kernel
+  // +28 ms (it now runs those long instances itself): +0.7 % end to end.  On the
+  // two-proposer shape (0.01 % bails) it only costs (-1 %): not used there.
+  static constexpr bool RSN = SL && PM * N > 18;
+  static constexpr int RC = RSN ? 5 : 4, RL = IB * RC, RLB = 3, RD = RL + RLB;
+  static constexpr int POOLB_SHIFT = RSN ? 1 : 0;    // entry e's pool word: POOLW - POOLB_SHIFT + e
   // compact layouts with a pool of <= 24 words: a Round2Success (no payload)
   // takes no pool word; its FIFO entry is the code RCB + (due & 7) instead
 #ifdef PXB_EV_NO_RCODE
@@ -112,7 +120,8 @@ struct Shape {
   static constexpr int WORDS = WHEEL + W * WW;
   static_assert(W == 4 || W == 8 || W == 16, "wheel of 4, 8 or 16 steps");
   static_assert(NIN <= 32 && NLQ <= 32, "masks are 32-bit");
-  static_assert(RD + 4 <= 32, "response-link word");
+  static_assert(RSN ? (IB * RC <= 32 && POOL < (1 << IB)) : (RD + 4 <= 32), "response-link word");
+  static constexpr int POOLB = POOLW - POOLB_SHIFT;
   static_assert(QL + QLB <= 31, "request-link word");
 };
 
@@ -123,7 +132,9 @@ struct Shape {
 //                       [30:28], reply seq in its own halfword)
 //   response-link word  pool index i (IB bits at IB*i); len [4IB+2:4IB]; last due&15 above it
 //                       (compact, pool <= 24: index 24 + (due & 7) = a Round2Success, no
-//                       pool word; dues stay within s + delay_max <= s + 4)
+//                       pool word; dues stay within s + delay_max <= s + 4;
+//                       slim over > 18 links: 5 entries of pool index + 1, 0 above the
+//                       length, nothing else)
 //   response word       x [11:0] | y [23:12] | z [25:24] | kind [31:30]
 //   broadcast payload   x [11:0] | z [13:12] | kind [15:14]
 //   acceptor word       t_max [11:0] | t_store [23:12] | val [25:24] | dead [26] | log_len [31:27]
@@ -176,6 +187,7 @@ __host__ __device__ __forceinline__ bool any_lane(bool p) {
 
 __host__ __device__ __forceinline__ uint32_t ctz32(uint32_t x) { return x ? (uint32_t)__builtin_ctz(x) : 32u; }
 __host__ __device__ __forceinline__ uint32_t popc32(uint32_t x) { return (uint32_t)__builtin_popcount(x); }
+__host__ __device__ __forceinline__ uint32_t nbits32(uint32_t x) { return x ? 32u - (uint32_t)__builtin_clz(x) : 0u; }
 
 // Per-instance outcome handed to the driver when a lane finishes.
 struct EvOut {
@@ -235,10 +247,12 @@ struct EvLane {
   uint32_t clog_len;
   bool bailed;
 
+  // (slim: bit e for pool word e - 1, bit 0 unused)
   __host__ __device__ static constexpr pool_mask_t full_pool() {
     return (POOL == 8 * (int)sizeof(pool_mask_t)) ? ~(pool_mask_t)0
-                                                   : (pool_mask_t)(((pool_mask_t)1 << (POOL % (8 * sizeof(pool_mask_t)))) - 1u);
+                                                   : (pool_mask_t)((((pool_mask_t)1 << (POOL % (8 * sizeof(pool_mask_t)))) - 1u) << S::POOLB_SHIFT);
   }
+  static_assert(POOL + S::POOLB_SHIFT <= 8 * (int)sizeof(pool_mask_t), "pool mask");
 
   // ---- selects over per-proposer / per-acceptor register arrays (index may differ per lane) ----
   // The operands go through an empty asm: otherwise LLVM folds the select
@@ -551,8 +565,17 @@ struct EvLane {
     const uint32_t Lq = ca * (uint32_t)PM + cp;
     const uint32_t lw = isR ? S::RSP + rp.Lr : S::REQ + Lq;   // the link word
     const uint32_t wv = m.ld(lw);
-    const uint32_t len = isR ? (wv >> S::RL) & RLM : (wv >> S::QL) & QLM;
-    const uint32_t tail = isR ? (wv >> S::RD) & 15u : (wv >> ((7u * len - 4u) & 31u)) & 15u;
+    uint32_t rlen, rtail;
+    if constexpr (S::RSN) {                          // (the tail entry's pool word holds its due)
+      rlen = (nbits32(wv) + (uint32_t)S::IB - 1u) / (uint32_t)S::IB;
+      const uint32_t te = (wv >> ((S::IB * rlen - S::IB) & 31u)) & (isR ? IM : 0u);
+      rtail = (m.ld(S::POOLB + te) >> 26) & 15u;
+    } else {
+      rlen = (wv >> S::RL) & RLM;
+      rtail = (wv >> S::RD) & 15u;
+    }
+    const uint32_t len = isR ? rlen : (wv >> S::QL) & QLM;
+    const uint32_t tail = isR ? rtail : (wv >> ((7u * len - 4u) & 31u)) & 15u;
     const uint32_t rel = (tail - b4) & (len ? 15u : 0u);
     const uint32_t due_rel = d > rel ? d : rel;
     const uint32_t due4 = (b4 + due_rel) & 15u;
@@ -563,7 +586,7 @@ struct EvLane {
                                     : ctz32((uint32_t)pfree) & 31u;
     // the pool word: to a free entry (harmless unless a reply goes), or, with
     // none free, to the link word, which the next store rewrites
-    m.st(pfree ? S::POOLW + k2 : lw, rp.pw | (due4 << 26));
+    m.st(pfree ? S::POOLB + k2 : lw, rp.pw | (due4 << 26));
     if constexpr (LG) {                              // (no free entry: the dummy halfword)
       const uint32_t zi = pfree ? k2 : (uint32_t)POOL;
       m.st16h(S::POOLZ + (zi >> 1), zi & 1u, rp.z);
@@ -571,7 +594,8 @@ struct EvLane {
     pfree &= (go & isR & !r2c) ? ~((pool_mask_t)1 << k2) : ~(pool_mask_t)0;
     const uint32_t ent = r2c ? S::RCB + (due4 & 7u) : k2;
     // (entries above a FIFO's length are 0: appends are additions)
-    const uint32_t nR = ((wv + (1u << S::RL) + (ent << (S::IB * len))) & ~(15u << S::RD)) | (due4 << S::RD);
+    const uint32_t nR = S::RSN ? wv | (ent << ((S::IB * len) & 31u))
+                               : ((wv + (1u << S::RL) + (ent << (S::IB * len))) & ~(15u << S::RD)) | (due4 << S::RD);
     const uint32_t nQ = wv + (1u << S::QL) + ((cslot | (due4 << 3)) << (7u * len));
     m.st(lw, go ? (isR ? nR : nQ) : wv);
     put(refc, cp, get(refc, cp) + ((go & !isR) ? 1u << (4u * cslot) : 0u));
@@ -788,14 +812,15 @@ struct EvLane {
       const uint32_t k = rr & IM, nk = (rr >> S::IB) & IM;
       // (a Round2Success code: no pool word, its due in the code)
       const bool kc = S::RCODE & (k >= S::RCB), nkc = S::RCODE & (nk >= S::RCB);
-      const uint32_t pe0 = m.ld(S::POOLW + (kc ? 0u : k));
-      const uint32_t pn = m.ld(S::POOLW + (nkc ? 0u : nk));
+      const uint32_t pe0 = m.ld(S::POOLB + (kc ? 0u : k));
+      const uint32_t pn = m.ld(S::POOLB + (nkc ? 0u : nk));
       const uint32_t pe = kc ? (R2S << 30) : pe0;
       pfree |= (resp & !kc) ? ((pool_mask_t)1 << k) : (pool_mask_t)0;
-      m.st(S::RSP + Lr, resp ? ((rr & ((1u << S::RL) - 1u)) >> S::IB) + ((rr & ~((1u << S::RL) - 1u)) - (1u << S::RL))
-                             : rr);                         // (popped: entries down one, length - 1)
+      const uint32_t popped = S::RSN ? rr >> S::IB
+                                     : ((rr & ((1u << S::RL) - 1u)) >> S::IB) + ((rr & ~((1u << S::RL) - 1u)) - (1u << S::RL));
+      m.st(S::RSP + Lr, resp ? popped : rr);         // (popped: entries down one, length - 1)
       const bool nnow = nkc ? ((nk & 7u) == (s4 & 7u)) : (((pn >> 26) & 15u) == s4);
-      const bool rkeep = resp & (rlen > 1u) & nnow;
+      const bool rkeep = resp & (S::RSN ? nk != 0u : rlen > 1u) & nnow;
       in_mask = (pin & !rkeep) ? (in_mask & ~(1u << j)) : in_mask;
       const uint32_t rkind = pe >> 30, px = pe & 0xFFFu, py = (pe >> 12) & 0xFFFu;
       const uint32_t pz = LG ? m.ld16h(S::POOLZ + (k >> 1), k & 1u) : (pe >> 24) & 3u;
@@ -915,7 +940,11 @@ struct EvLane {
   // messages queued on the links (the trace's in_flight; the kernels test the wheel)
   __host__ __device__ uint32_t links_in_flight() const {
     uint32_t n = 0u;
-    for (uint32_t L = 0; L < NLQ; ++L) n += ((m.ld(S::REQ + L) >> S::QL) & QLM) + ((m.ld(S::RSP + L) >> S::RL) & RLM);
+    for (uint32_t L = 0; L < NLQ; ++L) {
+      const uint32_t rw = m.ld(S::RSP + L);
+      n += ((m.ld(S::REQ + L) >> S::QL) & QLM)
+           + (S::RSN ? (nbits32(rw) + (uint32_t)S::IB - 1u) / (uint32_t)S::IB : (rw >> S::RL) & RLM);
+    }
     return n;
   }
 

@@ -69,10 +69,11 @@ struct EvKParams {
 // (log mode over at most 10 links: 18 words, which faulty log mode's batch never
 // fills (extra.log_mode_faulty: no bail in 20000 instances): 85 words per lane,
 // 7 waves per CU instead of 5)
-// (slim: 44 words hold the responses of 98.4 % of config 5's P = 3 instances,
-// 30 those of 99.99 % of its P = 2 ones; compact over <= 10 links: config 3
-// bails no more with 16 words than with 24, and its shape then leaves LDS to
-// spare at 12 waves per CU)
+// (slim: 44 words hold the responses of 99.6 % of config 5's P = 3 instances
+// (with its 5-deep response FIFOs, whose entries are pool index + 1: < 64
+// words), 30 those of 99.99 % of its P = 2 ones; compact over <= 10 links:
+// config 3 bails no more with 16 words than with 24, and its shape then leaves
+// LDS to spare at 12 waves per CU)
 template <int PM, int N, bool CMP, bool LG = false, bool SL = false>
 struct EvPool {
   static constexpr int value = (LG && PM * N <= 10)  ? 18
