@@ -149,6 +149,17 @@ def test_config5_8step_layouts(pm, layout, monkeypatch):
     check(pxb.CONFIGS[5], 3000, 1500, max_bail_frac=0.75 if pm == 2 else 0.03)
 
 
+def test_config5_three_proposer_deep_response_fifos(monkeypatch):
+    """The slim three-proposer shape's 5-deep response FIFOs (entries pool
+    index + 1, the tail's due read from its pool word): exact against the
+    oracle, and config 5 bails ~0.4 % of its P = 3 instances (1.7 % with
+    4-deep FIFOs, most of them on a full response FIFO)."""
+    monkeypatch.setenv("EV_LAYOUT", "5")
+    monkeypatch.setenv("EV_PM", "3")
+    _, _, bails = check(pxb.CONFIGS[5], 9000, 6000, max_bail_frac=0.003)
+    assert len(bails) > 0                            # (the pool and the rings still bail)
+
+
 @pytest.mark.parametrize("layout", [2, 3])
 @pytest.mark.parametrize("P", [1, 2, 3])
 @pytest.mark.parametrize("N", [2, 5, 9])
