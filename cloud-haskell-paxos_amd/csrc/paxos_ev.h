@@ -594,8 +594,9 @@ struct EvLane {
     pfree &= (go & isR & !r2c) ? ~((pool_mask_t)1 << k2) : ~(pool_mask_t)0;
     const uint32_t ent = r2c ? S::RCB + (due4 & 7u) : k2;
     // (entries above a FIFO's length are 0: appends are additions)
+    constexpr int RD = S::RSN ? 0 : S::RD;          // (no due field in a slim >18-link word)
     const uint32_t nR = S::RSN ? wv | (ent << ((S::IB * len) & 31u))
-                               : ((wv + (1u << S::RL) + (ent << (S::IB * len))) & ~(15u << S::RD)) | (due4 << S::RD);
+                               : ((wv + (1u << S::RL) + (ent << (S::IB * len))) & ~(15u << RD)) | (due4 << RD);
     const uint32_t nQ = wv + (1u << S::QL) + ((cslot | (due4 << 3)) << (7u * len));
     m.st(lw, go ? (isR ? nR : nQ) : wv);
     put(refc, cp, get(refc, cp) + ((go & !isR) ? 1u << (4u * cslot) : 0u));
