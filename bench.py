@@ -1,29 +1,27 @@
 """Benchmark: Paxos instances decided per second on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 4]
 
 One step = one pxb_run_device call over one batch of fresh synthetic
-instances.  The headline workload is BASELINE config 2 (1 proposer, 5
-acceptors, no faults; the single-GPU configuration the metric is quoted on):
-a step runs BATCHES_PER_STEP = 256 config-2 batches of 2^20 instances (2^28
-fresh global ids), so the default 20 steps time well over 100 ms.  Instances are generated on the
-device from (seed, global instance id), so the inputs are resident before the
-timed region; outputs (16 B result + 4 B/acceptor digest per instance) are
-written to HBM.
+instances.  The headline workload is the north star, BASELINE config 4: 2^26
+(64M) instances per step with 2 duelling proposers, 7 acceptors, delays in
+[1, 4] and seeded acceptor crash windows, split over the job's GPUs (strong
+scaling: 2^26 / N contiguous global ids per rank and step).  Instances are
+generated on the device from (seed, global instance id), so the inputs are
+resident before the timed region; outputs (16 B result + 4 B/acceptor digest
+per instance) are written to HBM.  `value` = decided instances / s over the
+whole job.
 
 For N > 1 (one process per GPU, torchrun) each rank runs its own instance
-ranges (weak scaling, no data-path collective) and the run totals (decided
-counts, violation flags) are summed with one RCCL all-reduce.  `--gpus N`
-without torchrun spawns the N ranks itself (a child torch.distributed.run,
-started before this process touches a GPU).  Prints ONE JSON line on rank 0.
-
-The line also carries the north-star workload (BASELINE config 4: 64M
-instances with seeded crash windows) with its own roofline: 2^26 instances
-split over the N ranks (strong scaling, 2^26 / N per GPU, barriers and the
-max-over-ranks time as above, totals all-reduced over RCCL).  On one GPU it
-also carries config 4 at 2^23 (the per-GPU share at N = 8), the other faulty
-configs at scale, log mode, and the CPU baseline (the oracle's C port on the
-host cores).
+range (no data-path collective) and the run totals (decided counts,
+violation flags) are summed with one RCCL all-reduce after the timed region.
+`--gpus N` without torchrun spawns the N ranks itself (a child
+torch.distributed.run, started before this process touches a GPU).  Prints
+ONE JSON line on rank 0: the headline first (with its roofline and the CPU
+baseline of the same config), then, on one GPU, `extra`: config 2 (the
+fault-free 2^28-instance batch, the round-1..3 headline), config 4 at 2^23 (the
+per-GPU share at N = 8), configs 3 and 5 at scale, config 5's whole 2^28 sweep
+(totals only), fault-free and faulty log mode, and the wire codec.
 """
 from __future__ import annotations
 
@@ -46,7 +44,7 @@ VALU_PEAK_G = CUS * 2 * 2.4  # G wave64 VALU instructions / s (1228.8)
 PROFILES = os.path.join(ROOT, "profiles")
 PROFILE_ROUNDS = ("r03", "r02")   # the newest committed profile set of a workload wins
 BATCHES_PER_STEP = 256       # config-2 batches of 2^20 per timed step (>= 100 ms over 20 steps)
-DRY_NORTH_STAR = 1 << 12     # --dry-run stand-in for the north star's 2^26 total
+DRY_NORTH_STAR = 1 << 12     # --dry-run stand-in for the headline's 2^26 instances per step
 
 
 def parse():
@@ -54,8 +52,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", type=int, default=2, choices=[2, 3, 4, 5, 6, 7],
-                    help="BASELINE config (6: log mode, 7: faulty log mode)")
+    ap.add_argument("--config", type=int, default=4, choices=[2, 3, 4, 5, 6, 7],
+                    help="BASELINE config (6: log mode, 7: faulty log mode).  Configs 4 and 5 are one "
+                         "batch over the job (2^26 and 2^28 instances per step, each rank 1/N of it: a "
+                         "one-GPU --config 5 run takes all 2^28 per step); config 2 is 2^28 per GPU")
     ap.add_argument("--instances", type=int, default=0, help="per GPU per step (default: the config's step size)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
@@ -98,13 +98,14 @@ class GpuLeg:
     """The measured work of one rank: pxb_run_device over fresh instance ids,
     asynchronous on one HIP stream, timed with an event pair on that stream."""
 
-    def __init__(self, cfg, n, rank, world, stream, dev):
+    def __init__(self, cfg, n, rank, world, stream, dev, outputs=True):
         import torch
         import pxb
         self.torch, self.pxb = torch, pxb
         self.cfg, self.n, self.rank, self.world, self.stream, self.dev = cfg, n, rank, world, stream, dev
-        self.out = torch.empty((n, 4), dtype=torch.int32, device=dev)
-        self.dig = torch.empty((n, cfg.n_acceptors), dtype=torch.int32, device=dev)
+        # (outputs=False: run totals only, no per-instance records)
+        self.out = torch.empty((n, 4), dtype=torch.int32, device=dev) if outputs else None
+        self.dig = torch.empty((n, cfg.n_acceptors), dtype=torch.int32, device=dev) if outputs else None
         self.tot = torch.zeros(16, dtype=torch.int64, device=dev)
         self.e0 = torch.cuda.Event(enable_timing=True)
         self.e1 = torch.cuda.Event(enable_timing=True)
@@ -337,11 +338,11 @@ def cpu_baseline(cfg, budget_s):
             "one_core": {"value": one / dt1, "sample": "%d further instances, 1 thread, %.1f s" % (one, dt1)}}
 
 
-def faulty_line(name, c, n, steps, warmup, stream, dev, warm_n, rank=0, world=1, leg=None):
-    """One faulty workload: n instances per rank per step, on every rank of the
-    job (barriers, max-over-ranks time, all-reduced totals: run_workload)."""
+def faulty_line(name, c, n, steps, warmup, stream, dev, warm_n, rank=0, world=1, leg=None, outputs=True):
+    """One workload: n instances per rank per step, on every rank of the job
+    (barriers, max-over-ranks time, all-reduced totals: run_workload)."""
     import pxb
-    leg = leg or GpuLeg(pxb.CONFIGS[c], n, rank, world, stream, dev)
+    leg = leg or GpuLeg(pxb.CONFIGS[c], n, rank, world, stream, dev, outputs=outputs)
     es, ek, ecnt = run_workload(leg, n, steps, warmup, world, warm_n=warm_n)
     line = {"workload": name, "instances_per_step": n * world, "instances_per_gpu_per_step": n, "n_gpus": world,
             "instances_per_s": ecnt["instances"] / es, "decided_per_s": ecnt["decided"] / es,
@@ -354,60 +355,60 @@ def faulty_line(name, c, n, steps, warmup, stream, dev, warm_n, rank=0, world=1,
     return line
 
 
-def north_star_line(rank, world, stream=None, dev=None, dry_total=0):
-    """BASELINE config 4 as the north star states it: 2^26 instances with
-    seeded crash windows sharded over the node's GPUs (2^26 / world per rank,
-    contiguous global-id ranges), strong scaling.  Every rank runs it."""
-    import pxb
-    total = dry_total or pxb.CONFIG_INSTANCES[4]
-    n = total // world
-    leg = DryLeg(n, rank, world) if dry_total else None
-    line = faulty_line("BASELINE config 4: 2^%d instances over %d GPU%s (%d per GPU)" % (
-                           total.bit_length() - 1, world, "s" if world > 1 else "", n),
-                       4, n, 1, 1, stream, dev, min(n, 1 << 22), rank=rank, world=world, leg=leg)
-    line["scaling"] = "strong"
-    line["rccl_world"] = world
-    return line
-
-
-def log_faulty_line(stream, dev, n=1 << 20):
+def log_faulty_line(stream, dev, n=1 << 22, general=True):
     """Faulty log mode (pxb.LOG_FAULTY_CONFIG: P = 2, N = 5, 10 % loss, delays
     to 4, crash windows, 16 Ticks 8 steps apart) on the per-lane kernel's
-    log-mode shape, and the same batch on the general kernel (PXB_NO_EV=1) for
-    the speed-up; the totals of the two must be identical."""
+    log-mode shape, and (general=True) the same batch on the general kernel
+    (PXB_NO_EV=1) for the speed-up; the totals of the two must be identical.
+    At 2^22 instances per step the kernel runs saturated; at 2^20 the chunk
+    tail (the slowest instances of the last waves) is a large share."""
     import pxb
     cfg = pxb.LOG_FAULTY_CONFIG
     es, ek, ecnt = run_workload(GpuLeg(cfg, n, 0, 1, stream, dev), n, 2, 1, 1)
-    os.environ["PXB_NO_EV"] = "1"
-    try:
-        gs, gk, gcnt = run_workload(GpuLeg(cfg, n, 0, 1, stream, dev), n, 2, 1, 1)
-    finally:
-        del os.environ["PXB_NO_EV"]
-    assert gcnt == ecnt, (gcnt, ecnt)
-    return {"workload": "faulty log mode: P=2, N=5, 10% loss, delay [1,4], crash windows, 16 Ticks / 8 steps",
+    line = {"workload": "faulty log mode: P=2, N=5, 10% loss, delay [1,4], crash windows, 16 Ticks / 8 steps",
             "instances_per_step": n, "instances_per_s": ecnt["instances"] / es,
             "commands_committed_per_s": ecnt["executes"] / es, "kernel_ms": ek,
-            "roofline": roofline("config7", n, ek, ecnt["canon_bytes"] / 2),
-            "general_kernel": {"instances_per_s": gcnt["instances"] / gs, "kernel_ms": gk},
-            "speedup_vs_general_kernel": gk / ek, "counters": ecnt}
+            "roofline": roofline("config7", n, ek, ecnt["canon_bytes"] / 2), "counters": ecnt}
+    if general:
+        os.environ["PXB_NO_EV"] = "1"
+        try:
+            gs, gk, gcnt = run_workload(GpuLeg(cfg, n, 0, 1, stream, dev), n, 2, 1, 1)
+        finally:
+            del os.environ["PXB_NO_EV"]
+        assert gcnt == ecnt, (gcnt, ecnt)
+        line["general_kernel"] = {"instances_per_s": gcnt["instances"] / gs, "kernel_ms": gk}
+        line["speedup_vs_general_kernel"] = gk / ek
+    return line
+
+
+def headline_workload(c, n, world):
+    if c == 4:
+        return ("BASELINE config 4 (north star): 2^26 instances per step, 2 duelling proposers, 7 acceptors, "
+                "delays [1,4], seeded crash windows, over %d GPU%s (%d per GPU)" % (world, "s" if world > 1 else "", n))
+    if c == 2:
+        return "BASELINE config 2: %d fresh instances per GPU per step (%d x the 2^20 batch)" % (n, n >> 20)
+    return "BASELINE config %d: %d instances per GPU per step" % (c, n)
 
 
 def dry_main(args, rank, world):
     """--dry-run: the N-rank launcher path on CPU (gloo); prints the JSON line
-    shape with a synthetic workload and "data": "dry-run" (not a measurement)."""
+    shape with a synthetic workload and "data": "dry-run" (not a measurement).
+    The headline is strong-scaled like config 4's: one batch of --instances
+    (default DRY_NORTH_STAR) per step split over the ranks."""
     import torch.distributed as dist
     if world > 1:
         dist.init_process_group("gloo")
-    n = args.instances or 1000
+    total = args.instances or DRY_NORTH_STAR
+    n = total // world
     secs, kms, cnt = run_workload(DryLeg(n, rank, world), n, args.steps, args.warmup, world)
     assert cnt["instances"] == n * world * args.steps, cnt
-    ns = None if args.no_extra else north_star_line(rank, world, dry_total=DRY_NORTH_STAR)
     if rank == 0:
-        line = {"metric": "dry-run", "value": cnt["decided"] / secs, "n_gpus": world, "steps": args.steps,
-                "warmup": args.warmup, "ms_per_step": secs / args.steps * 1e3, "data": "dry-run",
-                "rccl_world": world, "counters": cnt}
-        if ns:
-            line["north_star"] = ns
+        line = {"metric": "dry-run", "value": cnt["decided"] / secs, "unit": "instances/s", "n_gpus": world,
+                "steps": args.steps, "warmup": args.warmup, "ms_per_step": secs / args.steps * 1e3,
+                "scaling": "strong", "data": "dry-run",
+                "config": {"workload": headline_workload(4, n, world), "instances_per_step": n * world,
+                           "instances_per_gpu_per_step": n, "rccl_world": world},
+                "counters": cnt}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -436,9 +437,12 @@ def main():
     cfg = pxb.CONFIGS[c]
     n = step_instances(c, args.instances, world)
 
+    # the headline: K timed steps of n fresh instances per rank (BASELINE
+    # config 4 by default: 2^26 / N per rank, strong scaling)
     secs, kms, cnt = run_workload(GpuLeg(cfg, n, rank, world, stream, dev), n, args.steps, args.warmup, world)
     total_inst = n * world * args.steps
     assert cnt["instances"] == total_inst, cnt
+    assert cnt["decided"] + cnt["undecided"] == total_inst, cnt
     if c == 2:   # closed forms of the fault-free config: every instance decides
         assert cnt["decided"] == total_inst and cnt["canon_bytes"] == 1140 * total_inst, cnt
     value = cnt["decided"] / secs                         # decided instances / s, whole job
@@ -455,33 +459,43 @@ def main():
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic (Philox4x32-10 schedule from seed + global instance id)",
-        "config": {"workload": "BASELINE config %d" % c + (
-                       ": %d fresh instances per GPU per step (%d x the 2^20 batch)" % (n, n >> 20) if c == 2 else ""),
-                   "instances_per_gpu_per_step": n,
+        "config": {"workload": headline_workload(c, n, world),
+                   "instances_per_step": n * world, "instances_per_gpu_per_step": n,
                    "proposers": cfg.n_proposers, "acceptors": cfg.n_acceptors,
                    "loss_ppm": cfg.loss_ppm, "delay_max": cfg.delay_max, "skew_max": cfg.skew_max,
                    "crash_ppm": cfg.crash_ppm, "step_cap": cfg.step_cap,
                    "randomize": cfg.randomize, "seed": hex(cfg.seed),
                    "parallelism": "instance-range shards x%d" % world, "rccl_world": world},
+        "instances_per_s": cnt["instances"] / secs,
+        "kernel_ms_per_step": kms,
         "roofline": roofline("config%d" % c, n, kms, cnt["canon_bytes"] / (args.steps * world)),
         "counters": cnt,
     }
-    if not args.no_extra and c == 2:
-        # the north star: BASELINE config 4 (64M instances, 2 duelling proposers,
-        # 7 acceptors, seeded crash windows) over this job's GPUs, every rank
-        line["north_star"] = north_star_line(rank, world, stream, dev)
-    if rank == 0 and not args.no_extra and c == 2 and world == 1:
+    if rank == 0 and world == 1 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
+    if rank == 0 and not args.no_extra and c == 4 and world == 1:
         extra = {}
+        # config 2 (fault-free, 1 proposer, 5 acceptors): 2^28 fresh instances
+        # per step, the round 1-3 headline
+        extra["config2"] = faulty_line(headline_workload(2, step_instances(2, 0), 1), 2, step_instances(2, 0),
+                                       10, 1, stream, dev, None)
+        if not args.no_cpu:
+            extra["config2"]["cpu_baseline"] = cpu_baseline(pxb.CONFIGS[2], 3.0)
         # config 4 at its per-GPU share at N = 8 (2^23): the chunk-tail cost at
         # that size, before any 8-GPU run
         extra["config4_share"] = faulty_line("BASELINE config 4: 2^23 instances (the per-GPU share of 2^26 "
-                                             "over 8 GPUs) on 1 GPU", 4, pxb.CONFIG_INSTANCES[4] // 8, 2, 1,
+                                             "over 8 GPUs) on 1 GPU", 4, pxb.CONFIG_INSTANCES[4] // 8, 4, 1,
                                              stream, dev, 1 << 22)
         extra["config3"] = faulty_line("BASELINE config 3: 2^24 instances", 3, pxb.CONFIG_INSTANCES[3],
                                        2, 1, stream, dev, 1 << 22)
         extra["config5"] = faulty_line("BASELINE config 5: 2^25 instances (the per-GPU share of 2^28 "
                                        "over 8 GPUs)", 5, pxb.CONFIG_INSTANCES[5] // 8, 1, 1, stream, dev,
                                        1 << 22)
+        # config 5 at its stated size: the whole 2^28-schedule sweep on this
+        # one GPU, run totals only (agreement-violation flags summed)
+        extra["config5_full"] = faulty_line("BASELINE config 5: all 2^28 randomized schedules on 1 GPU, "
+                                            "run totals only", 5, pxb.CONFIG_INSTANCES[5], 1, 0, stream, dev,
+                                            None, outputs=False)
         extra["wire_codec"] = wire_bench(stream, dev)
         # log mode: stock Main.hs topology with the ticker running (SEMANTICS §9)
         en = 1 << 20
@@ -489,12 +503,9 @@ def main():
         extra["log_mode"] = {"instances_per_step": en, "ticks_per_proposer": pxb.LOG_CONFIG.n_ticks,
                              "commands_committed_per_s": ecnt["executes"] / es,
                              "instances_per_s": ecnt["instances"] / es, "kernel_ms": ek, "counters": ecnt}
-        extra["log_mode_faulty"] = log_faulty_line(stream, dev)
+        extra["log_mode_faulty"] = log_faulty_line(stream, dev, 1 << 22)
+        extra["log_mode_faulty_2p20"] = log_faulty_line(stream, dev, 1 << 20, general=False)
         line["extra"] = extra
-    if rank == 0 and world == 1 and not args.no_cpu:
-        line["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
-        if "north_star" in line:
-            line["north_star"]["cpu_baseline"] = cpu_baseline(pxb.CONFIGS[4], min(args.cpu_seconds, 8.0))
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -122,17 +122,17 @@ __global__ __launch_bounds__(TCOPIES) void finalize_kernel(unsigned long long* p
 typedef void (*kernel_ptr)(KParams);
 typedef void (*ev_kernel_ptr)(ev::EvKParams);
 
-template <int PM, int W, bool C, bool L = false, bool S = false>
+template <int PM, int W, bool C, bool L = false, bool S = false, bool SP = false>
 static ev_kernel_ptr ev_pick_n(uint32_t n) {
   switch (n) {
-    case 2: return ev::paxos_ev_kernel<PM, 2, W, C, L, S>;
-    case 3: return ev::paxos_ev_kernel<PM, 3, W, C, L, S>;
-    case 4: return ev::paxos_ev_kernel<PM, 4, W, C, L, S>;
-    case 5: return ev::paxos_ev_kernel<PM, 5, W, C, L, S>;
-    case 6: return ev::paxos_ev_kernel<PM, 6, W, C, L, S>;
-    case 7: return ev::paxos_ev_kernel<PM, 7, W, C, L, S>;
-    case 8: return ev::paxos_ev_kernel<PM, 8, W, C, L, S>;
-    case 9: return ev::paxos_ev_kernel<PM, 9, W, C, L, S>;
+    case 2: return ev::paxos_ev_kernel<PM, 2, W, C, L, S, SP>;
+    case 3: return ev::paxos_ev_kernel<PM, 3, W, C, L, S, SP>;
+    case 4: return ev::paxos_ev_kernel<PM, 4, W, C, L, S, SP>;
+    case 5: return ev::paxos_ev_kernel<PM, 5, W, C, L, S, SP>;
+    case 6: return ev::paxos_ev_kernel<PM, 6, W, C, L, S, SP>;
+    case 7: return ev::paxos_ev_kernel<PM, 7, W, C, L, S, SP>;
+    case 8: return ev::paxos_ev_kernel<PM, 8, W, C, L, S, SP>;
+    case 9: return ev::paxos_ev_kernel<PM, 9, W, C, L, S, SP>;
   }
   return nullptr;
 }
@@ -172,7 +172,8 @@ static ffp_kernel_ptr ffp_pick(uint32_t p, uint32_t n) {
 }
 
 // layout index: 0 = 8-step wheel, 1 = 16-step wheel, 2 / 3 = compact links (8- / 4-step wheel),
-// 4 = log mode (8-step wheel), 5 = slim (8-step wheel, byte reply seqs: ev::layout_for)
+// 4 = log mode (8-step wheel), 5 = slim (8-step wheel, byte reply seqs), 6 = layout 3 for
+// simple schedules (no loss, no Tick skew: ev::layout_for)
 static ev_kernel_ptr ev_pick(uint32_t pm, uint32_t n, int layout) {
   switch (pm * 10 + (uint32_t)layout) {
     case 10: return ev_pick_n<1, 8, false>(n);
@@ -181,18 +182,21 @@ static ev_kernel_ptr ev_pick(uint32_t pm, uint32_t n, int layout) {
     case 13: return ev_pick_n<1, 4, true>(n);
     case 14: return ev_pick_n<1, 8, false, true>(n);
     case 15: return ev_pick_n<1, 8, false, false, true>(n);
+    case 16: return ev_pick_n<1, 4, true, false, false, true>(n);
     case 20: return ev_pick_n<2, 8, false>(n);
     case 21: return ev_pick_n<2, 16, false>(n);
     case 22: return ev_pick_n<2, 8, true>(n);
     case 23: return ev_pick_n<2, 4, true>(n);
     case 24: return ev_pick_n<2, 8, false, true>(n);
     case 25: return ev_pick_n<2, 8, false, false, true>(n);
+    case 26: return ev_pick_n<2, 4, true, false, false, true>(n);
     case 30: return ev_pick_n<3, 8, false>(n);
     case 31: return ev_pick_n<3, 16, false>(n);
     case 32: return ev_pick_n<3, 8, true>(n);
     case 33: return ev_pick_n<3, 4, true>(n);
     case 34: return ev_pick_n<3, 8, false, true>(n);
     case 35: return ev_pick_n<3, 8, false, false, true>(n);
+    case 36: return ev_pick_n<3, 4, true, false, false, true>(n);
   }
   return nullptr;
 }
@@ -285,7 +289,7 @@ struct EvLists {
 };
 static EvLists g_lists[64][EV_LIST_STREAMS];
 static int g_nlists[64], g_lnext[64];
-static int g_eocc[6][4][10][64];
+static int g_eocc[7][4][10][64];
 static int g_ff1occ[10][64];
 static int g_ffpocc[4][10][64];
 

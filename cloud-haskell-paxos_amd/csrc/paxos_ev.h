@@ -66,9 +66,10 @@ static_assert(MAX_STEP_CAP < PXB_TICKET_LIMIT, "EV tickets never reach the overf
 // lane modes
 constexpr uint32_t M_IDLE = 0, M_RUN = 1;
 
-template <int PM_, int N_, int POOL_, int W_, bool CMP_, bool LG_ = false, bool SL_ = false>
+template <int PM_, int N_, int POOL_, int W_, bool CMP_, bool LG_ = false, bool SL_ = false, bool SP_ = false>
 struct Shape {
   static constexpr int PM = PM_, N = N_, POOL = POOL_, W = W_;
+  static constexpr bool SP = SP_;                    // simple schedule: no loss, no Tick skew, single decree
   static constexpr bool CMP = CMP_;                  // compact links (see Layouts)
   static constexpr bool LG = LG_;                    // log mode (several Ticks, long logs; see Layouts)
   static constexpr bool SL = SL_;                    // slim 4-entry layout (see Layouts)
@@ -185,6 +186,19 @@ __host__ __device__ __forceinline__ bool any_lane(bool p) {
 #endif
 }
 
+// Host-only probes (tools/wave_model.cpp): which wave-level branches and slots
+// a lane uses in an iteration.  Nothing on the device.
+enum : uint32_t {
+  EVP_END = 1u << 0, EVP_FIN = 1u << 1, EVP_RUN = 1u << 2, EVP_TICK_ENTER = 1u << 3, EVP_TICK_END = 1u << 4,
+  EVP_ACC = 1u << 5, EVP_PROP = 1u << 6, EVP_COPY = 1u << 7, EVP_SEND1 = 1u << 8, EVP_BCAST = 1u << 9,
+};
+#if defined(PXB_EV_PROBES) && !defined(__HIP_DEVICE_COMPILE__)
+extern thread_local uint32_t ev_probe_bits;
+#define PXB_EV_PROBE(b, c) (ev_probe_bits |= (c) ? (uint32_t)(b) : 0u)
+#else
+#define PXB_EV_PROBE(b, c) ((void)0)
+#endif
+
 __host__ __device__ __forceinline__ uint32_t ctz32(uint32_t x) { return x ? (uint32_t)__builtin_ctz(x) : 32u; }
 __host__ __device__ __forceinline__ uint32_t popc32(uint32_t x) { return (uint32_t)__builtin_popcount(x); }
 __host__ __device__ __forceinline__ uint32_t nbits32(uint32_t x) { return x ? 32u - (uint32_t)__builtin_clz(x) : 0u; }
@@ -199,9 +213,10 @@ struct EvOut {
 // EARLY: a step may end with the copies of its last broadcast still to send
 // (see end_op); the trace kernel turns it off so that its per-step records
 // hold every message of the step in flight, as the oracle's do.
-template <int PM, int N, int POOL, int W, bool CMP, class Mem, bool EARLY = true, bool LG = false, bool SL = false>
+template <int PM, int N, int POOL, int W, bool CMP, class Mem, bool EARLY = true, bool LG = false, bool SL = false,
+          bool SP = false>
 struct EvLane {
-  using S = Shape<PM, N, POOL, W, CMP, LG, SL>;
+  using S = Shape<PM, N, POOL, W, CMP, LG, SL, SP>;
   // acceptor fields (Layouts): dead bit, log-length shift (LG: in accv) and its limit
   static constexpr uint32_t A_DEAD = LG ? 24 : 26, A_LEN = LG ? 14 : 27, A_LEN_MAX = LG ? (1u << 18) - 1u : 31;
   using pool_mask_t = typename std::conditional<(POOL > 32), unsigned long long, uint32_t>::type;
@@ -218,6 +233,8 @@ struct EvLane {
   uint32_t lo, hi;                    // global instance id (Philox counter words 0, 1)
   uint32_t P, dmax, loss_m1;
   bool lossy;
+  // (SP: loss-free batches, whose sends never test a loss draw)
+  static constexpr bool kLossy = !SP;
   int32_t s, last_tick;
   uint32_t acc_mask;                  // this step's request links with due messages left
   uint32_t in_mask;                   // this step's proposer inputs left (Tick / response links)
@@ -366,7 +383,7 @@ struct EvLane {
   __host__ __device__ __forceinline__ void enter(int32_t t) {
     s = t;
     pq_old = pq_len != 0u;                           // (only ever one: end_op)
-    canon0 = pq_old ? canon : canon - 1u;
+    if constexpr (!SP) canon0 = pq_old ? canon : canon - 1u;   // (SP: see end_op)
     const uint32_t slot = (uint32_t)t & WM;
     uint32_t wq, wi;
     if (S::WW == 1) {
@@ -383,7 +400,8 @@ struct EvLane {
     acc_mask = wq;
     // Ticks only up to the last skew
     uint32_t tk = 0u;
-    if (any_lane(t <= last_tick)) {                 // (single decree: the first steps only)
+    PXB_EV_PROBE(EVP_TICK_ENTER, t <= last_tick);
+    if (!SP && any_lane(t <= last_tick)) {          // (single decree: the first steps only; SP: init)
       opaque_barrier();
       tk = (t <= last_tick) ? ticks_at(t) : 0u;
       if constexpr (LG) {                            // the next Tick of each proposer that ticked
@@ -405,16 +423,40 @@ struct EvLane {
   __host__ __device__ __forceinline__ void set_keys(const EvParams& kp) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
+#if defined(PXB_EV_SGPR_KEYS) && defined(__HIP_DEVICE_COMPILE__)
+      // (A/B: the keys as SGPRs)
+      uint32_t a = kp.k0 + (uint32_t)r * 0x9E3779B9u, b = kp.k1 + (uint32_t)r * 0xBB67AE85u;
+      __asm__ volatile("" : "+s"(a));
+      __asm__ volatile("" : "+s"(b));
+      rk[2 * r] = a;
+      rk[2 * r + 1] = b;
+#else
       rk[2 * r] = opaque(kp.k0 + (uint32_t)r * 0x9E3779B9u);
       rk[2 * r + 1] = opaque(kp.k1 + (uint32_t)r * 0xBB67AE85u);
+#endif
     }
   }
   __host__ __device__ __forceinline__ uint4 draw(uint32_t c2, uint32_t c3) const {
     return philox_rk(lo, hi, c2, c3, rk);
   }
 
+  // the isolation window of acceptor a of global instance (lo, hi) given its
+  // draw w (SEMANTICS §4): c0 | c1 << 16, both clamped to 4096 (0: none)
+  __host__ __device__ static __forceinline__ uint32_t window_of(const EvParams& kp, const uint4& w, uint32_t crash_m1) {
+    uint32_t c0 = 0, c1 = 0;
+    if (w.x <= crash_m1) {
+      c0 = mulhi_n(w.y, kp.crash_start_max + 1u);
+      c1 = c0 + 1u + mulhi_n(w.z, kp.crash_len_max);
+    }
+    c0 = c0 < 4096u ? c0 : 4096u;
+    c1 = c1 < 4096u ? c1 : 4096u;
+    return c0 | (c1 << 16);
+  }
+
   // ---- instance start: parameters, Tick skews, isolation windows (SEMANTICS §4) ----
-  __host__ __device__ __forceinline__ void init(const EvParams& kp, uint32_t g) {
+  // (pre_win: the windows drawn elsewhere, by the wave's lanes together
+  // (paxos_ev_kernel.h); valid only for batches with a launch-wide crash rate)
+  __host__ __device__ __forceinline__ void init(const EvParams& kp, uint32_t g, const uint32_t* pre_win = nullptr) {
     gid = g;
     const uint64_t inst = kp.first_instance + g;
     lo = (uint32_t)inst;
@@ -453,17 +495,8 @@ struct EvLane {
     }
 #pragma unroll
     for (int a = 0; a < N; ++a) {
-      uint32_t c0 = 0, c1 = 0;
-      if (crashy) {
-        const uint4 w = draw(0u, (3u << 24) | (uint32_t)a);
-        if (w.x <= crash_m1) {
-          c0 = mulhi_n(w.y, kp.crash_start_max + 1u);
-          c1 = c0 + 1u + mulhi_n(w.z, kp.crash_len_max);
-        }
-      }
-      c0 = c0 < 4096u ? c0 : 4096u;
-      c1 = c1 < 4096u ? c1 : 4096u;
-      win[a] = c0 | (c1 << 16);
+      if (pre_win) win[a] = pre_win[a];
+      else win[a] = crashy ? window_of(kp, draw(0u, (3u << 24) | (uint32_t)a), crash_m1) : 0u;
       accw[a] = 0u;
       if constexpr (LG) accv[a] = 0u;
       accd[a] = 0x811C9DC5u;
@@ -488,6 +521,23 @@ struct EvLane {
     bailed = P > (uint32_t)PM;
     mode = M_RUN;
     enter(0);
+    if constexpr (SP) {
+      // Skew-free single decree: every proposer's only Tick is at step 0; it
+      // is handled here (handleTick, Client.hs:196-207: Idle -> Round1 with
+      // ticket 1, command c<id>, AskForTicket broadcast), so the proposer op
+      // never sees one.  Its copies go out over the next iterations in the
+      // order the proposer op would have queued them (proposer 0 first).
+#pragma unroll
+      for (int p = 0; p < PM; ++p) {
+        if ((uint32_t)p < P) {
+          canon += 48u;                              // (the Tick: a proposer input of step 0)
+          pw0[p] = 1u | (ROUND1 << 28);
+          pw1[p] = ((uint32_t)p + 1u) << 4;
+          broadcast((uint32_t)p, ASK, 1u, 0u, true, 1u, false, 0u);
+        }
+      }
+      in_mask = 0u;
+    }
   }
 
   // The handler's broadcasts (kind0, x0, z0) [and the restart's AskForTicket
@@ -507,6 +557,7 @@ struct EvLane {
     // a ring slot still referenced by a queued copy
     // (non-short-circuit: || here became two exec-mask branches)
     bailed = bailed | (p0 & (((rc >> (4u * slot0)) & 15u) != 0u)) | (p1 & (((rc >> (4u * slot1)) & 15u) != 0u));
+    PXB_EV_PROBE(EVP_BCAST, p0);
     if (p0) {                                        // (p1 only with p0)
       if constexpr (LG) {
         m.st(S::BRING + q * S::BR + slot0, x0 | (z0 << 12) | (kind0 << 30));
@@ -557,7 +608,8 @@ struct EvLane {
       put(nsent, cp, ck + (wrap ? 1u : 0u));
     }
     const bool snd = isR | csnd;
-    const bool ok = !(lossy & (w.x <= loss_m1));
+    PXB_EV_PROBE(EVP_SEND1, snd);
+    const bool ok = !(kLossy & lossy & (w.x <= loss_m1));
     const uint32_t d = 1u + mulhi_n(w.y, dmax);
     const bool go = snd & ok;
     const uint32_t base = isR ? (uint32_t)s : sb;   // the send step (a carried copy's is s - 1)
@@ -619,6 +671,7 @@ struct EvLane {
     const uint32_t sb = (uint32_t)s - (pq_old ? 1u : 0u);
     const uint32_t s4 = sb & 15u;
     const bool snd = act & (pq_len != 0u);
+    PXB_EV_PROBE(EVP_COPY, snd);
     const uint32_t ce = pq & 31u;
     const uint32_t cp = ce >> 3, cslot = ce & 7u, ca = acur;
     const uint32_t ck = get(nsent, cp);
@@ -632,7 +685,7 @@ struct EvLane {
       put(nsent, cp, ck + (wrap ? 1u : 0u));
     }
     // (w: the draw of copy_ctr() taken before this call)
-    const bool ok = !(lossy & (w.x <= loss_m1));
+    const bool ok = !(kLossy & lossy & (w.x <= loss_m1));
     const uint32_t d = 1u + mulhi_n(w.y, dmax);      // (delay_max <= 1: always 1)
     // enqueue (predicated: inactive lanes store to the dummy word)
     const bool go = snd & ok;
@@ -696,6 +749,7 @@ struct EvLane {
                                                    uint32_t ready) {
     const uint32_t s4 = (uint32_t)s & 15u;
     const bool acc = act & (ready != 0u);
+    PXB_EV_PROBE(EVP_ACC, acc);
     const uint32_t L = acc ? ctz32(ready) : 0u;
     const uint32_t a = L / (uint32_t)PM, p = L - a * (uint32_t)PM;
     const uint32_t wq = m.ld(S::REQ + L);
@@ -743,6 +797,7 @@ struct EvLane {
     const uint32_t nt_store = accept ? x : (run ? 0u : t_store);
     const uint32_t nval = accept ? z : (run ? 0u : val);
     lflags |= panic ? (uint32_t)PXB_F_PANIC : 0u;
+    PXB_EV_PROBE(EVP_RUN, run);
     if (__builtin_expect(run, 0)) {                  // executed <>= [c]: log, digest, divergence
       if (log_len >= A_LEN_MAX) bailed = true;
       put(accd, a, fnv_u32(get(accd, a), code_of(val)));
@@ -801,6 +856,7 @@ struct EvLane {
   __host__ __device__ __forceinline__ void prop_op(const EvParams& kp, bool act) {
     const uint32_t s4 = (uint32_t)s & 15u;
     const bool pin = act & (in_mask != 0u) & (pq_len + 2u <= PQ_CAP);
+    PXB_EV_PROBE(EVP_PROP, pin);
     {
       const uint32_t j = pin ? ctz32(in_mask) : 0u;
       const uint32_t q = j / (uint32_t)(N + 1);
@@ -841,9 +897,10 @@ struct EvLane {
       bool b1 = false;                                // the restart's AskForTicket (Client.hs:185)
       const uint32_t maj = (uint32_t)N >> 1;          // haveMajority: acks > floor(N/2), :191-194
       // the input's kind (response kinds 0-2, 3 = Tick, 4 = none) with the state, as one key
-      const uint32_t key = (pin ? (r == 0u ? 3u : rkind) : 4u) * 4u + R;
+      // (SP: no Tick after init)
+      const uint32_t key = (pin ? ((!SP && r == 0u) ? 3u : rkind) : 4u) * 4u + R;
       // handleTick, Client.hs:196-207
-      const bool t_go = key == 3u * 4u + IDLE;
+      const bool t_go = !SP && key == 3u * 4u + IDLE;
       // HaveTicket (state Round1 or Round2), :128-140
       const bool h_go = (key - (HAVE * 4u + ROUND1) < 2u) & (px >= T);
       // Round1OK, :142-170
@@ -896,21 +953,26 @@ struct EvLane {
   }
   __host__ __device__ __forceinline__ bool end_op(const EvParams& kp, EvOut& o, bool act) {
     if (act && end_ready(kp)) {
+      PXB_EV_PROBE(EVP_END, true);
       // (no message in flight: every queued one falls due after s and holds a
       // bit of its due step's wheel slot, which only entering that step clears)
-      const bool quiet = (pq_len == 0u) & (occ == 0u) & (s >= last_tick);
+      const bool quiet = (pq_len == 0u) & (occ == 0u) & (SP || s >= last_tick);
       // nothing but lost copies at a carried-over step: the instance was quiet at s - 1
-      const bool back = EARLY & (canon == canon0);
+      // (SP: never at a quiet step -- without loss, the carried copies sent
+      // at s were handled at s (canonical bytes) or hold a wheel slot)
+      const bool back = EARLY & !SP & (canon == canon0);
       // the next step with a due message or a Tick (skews of absent proposers are 0)
       const uint32_t s1 = (uint32_t)s + 1u;
       const uint32_t rot = ((occ >> (s1 & WM)) | (occ << ((W - (s1 & WM)) & WM))) & ((1u << W) - 1u);
       uint32_t nx = ((occ != 0u) & (pq_len == 0u)) ? s1 + ctz32(rot) : (pq_len ? s1 : 0xFFFFu);
-      if (any_lane(s < last_tick)) {                  // (a later Tick: first steps only)
+      PXB_EV_PROBE(EVP_TICK_END, s < last_tick);
+      if (!SP && any_lane(s < last_tick)) {           // (a later Tick: first steps only)
         opaque_barrier();
 #pragma unroll
         for (int q = 0; q < PM; ++q) nx = ((skew[q] > (uint32_t)s) & (skew[q] < nx)) ? skew[q] : nx;
       }
       const bool capped = !quiet & (nx >= kp.step_cap);
+      PXB_EV_PROBE(EVP_FIN, quiet | capped);
       if (__builtin_expect(quiet | capped, 0)) {
         s = capped ? (int32_t)kp.step_cap - 1 : (back ? s - 1 : s);
         finish(capped, o);
@@ -1025,15 +1087,16 @@ __host__ inline int layout_for(const pxb_config* c) {
   if (c->n_ticks > 1) return 4;                      // log mode: 8-step wheel, 4-entry FIFOs, LG fields
   if (!(c->flags & PXB_CFG_RANDOMIZE) && c->delay_max <= 4 && c->step_cap <= 512 &&
       c->n_proposers * c->n_acceptors <= 16)
-    return 3;
+    return (c->loss_ppm == 0 && c->skew_max == 0) ? 6 : 3;   // 6: layout 3, simple schedule (Shape::SP)
   if (wheel_for(c->delay_max) != 8) return 1;
 #ifndef PXB_EV_NO_SLIM
   if (c->step_cap <= 512) return 5;                  // slim: byte reply seqs suffice
 #endif
   return 0;
 }
-__host__ inline int layout_wheel(int layout) { return layout == 1 ? 16 : layout == 3 ? 4 : 8; }
-__host__ inline bool layout_compact(int layout) { return layout == 2 || layout == 3; }
+__host__ inline int layout_wheel(int layout) { return layout == 1 ? 16 : (layout == 3 || layout == 6) ? 4 : 8; }
+__host__ inline bool layout_compact(int layout) { return layout == 2 || layout == 3 || layout == 6; }
+__host__ inline bool layout_simple(int layout) { return layout == 6; }
 __host__ inline bool layout_log(int layout) { return layout == 4; }
 
 }  // namespace ev

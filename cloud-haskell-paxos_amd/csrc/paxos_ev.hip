@@ -12,15 +12,16 @@
 
 namespace pxb {
 namespace ev {
-#define PXB_EV_INST(N, W, C, L, S) template __global__ void paxos_ev_kernel<PXB_EV_P, N, W, C, L, S>(EvKParams);
-#define PXB_EV_FOR_N(W, C, L, S) PXB_EV_INST(2, W, C, L, S) PXB_EV_INST(3, W, C, L, S) PXB_EV_INST(4, W, C, L, S) \
-  PXB_EV_INST(5, W, C, L, S) PXB_EV_INST(6, W, C, L, S) PXB_EV_INST(7, W, C, L, S) PXB_EV_INST(8, W, C, L, S) \
-  PXB_EV_INST(9, W, C, L, S)
-PXB_EV_FOR_N(8, false, false, false)
-PXB_EV_FOR_N(16, false, false, false)
-PXB_EV_FOR_N(8, true, false, false)
-PXB_EV_FOR_N(4, true, false, false)
-PXB_EV_FOR_N(8, false, true, false)     // log mode
-PXB_EV_FOR_N(8, false, false, true)     // slim
+#define PXB_EV_INST(N, W, C, L, S, SP) template __global__ void paxos_ev_kernel<PXB_EV_P, N, W, C, L, S, SP>(EvKParams);
+#define PXB_EV_FOR_N(W, C, L, S, SP) PXB_EV_INST(2, W, C, L, S, SP) PXB_EV_INST(3, W, C, L, S, SP) \
+  PXB_EV_INST(4, W, C, L, S, SP) PXB_EV_INST(5, W, C, L, S, SP) PXB_EV_INST(6, W, C, L, S, SP) \
+  PXB_EV_INST(7, W, C, L, S, SP) PXB_EV_INST(8, W, C, L, S, SP) PXB_EV_INST(9, W, C, L, S, SP)
+PXB_EV_FOR_N(8, false, false, false, false)
+PXB_EV_FOR_N(16, false, false, false, false)
+PXB_EV_FOR_N(8, true, false, false, false)
+PXB_EV_FOR_N(4, true, false, false, false)
+PXB_EV_FOR_N(4, true, false, false, true)      // simple schedule (layout 6)
+PXB_EV_FOR_N(8, false, true, false, false)     // log mode
+PXB_EV_FOR_N(8, false, false, true, false)     // slim
 }  // namespace ev
 }  // namespace pxb

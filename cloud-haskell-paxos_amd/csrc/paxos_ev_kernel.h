@@ -129,16 +129,16 @@ struct EvTotals {
 // on some SIMDs: its register budget is then 168 VGPRs, which the second
 // bound (minimum waves per SIMD) makes the compiler keep to.
 // The slim layout fits 5 or more waves per CU, 2 on some SIMDs: <= 256 VGPRs.
-template <int PM, int N, int W, bool CMP, bool LG = false, bool SL = false>
+template <int PM, int N, int W, bool CMP, bool LG = false, bool SL = false, bool SP = false>
 __global__ __launch_bounds__(64, CMP ? 3 : SL ? 2 : 1) void paxos_ev_kernel(EvKParams kp) {
   constexpr int POOL = EvPool<PM, N, CMP, LG, SL>::value;
-  using S = Shape<PM, N, POOL, W, CMP, LG, SL>;
+  using S = Shape<PM, N, POOL, W, CMP, LG, SL, SP>;
   __shared__ uint32_t lds[S::WORDS * 64];
   const uint32_t lane = threadIdx.x;
   unsigned long long* const trow = kp.part + (size_t)(blockIdx.x % EV_TCOPIES) * 16u;
   EvTotals tot;
   tot.clear();
-  EvLane<PM, N, POOL, W, CMP, LdsMem, true, LG, SL> L;
+  EvLane<PM, N, POOL, W, CMP, LdsMem, true, LG, SL, SP> L;
   L.m = LdsMem{lds, lane};
   L.set_keys(kp.p);
   L.mode = M_IDLE;
@@ -156,6 +156,18 @@ __global__ __launch_bounds__(64, CMP ? 3 : SL ? 2 : 1) void paxos_ev_kernel(EvKP
   for (;;) {
     // ---- refill idle lanes from the wave's chunk of the queue ----
     uint64_t freeb = __builtin_amdgcn_ballot_w64(L.mode == M_IDLE);
+#ifndef PXB_EV_REFILL_MIN
+#define PXB_EV_REFILL_MIN 2
+#endif
+#if PXB_EV_REFILL_MIN > 1
+    // A refill runs only once two lanes are idle (or none is live): a refill
+    // costs the wave ~600 instructions whether it starts one lane or several,
+    // and a lane ends every ~17 wave-iterations (config 4), so nearly every
+    // refill started one lane.  Waiting for a second costs each instance ~8
+    // idle lane-iterations of its ~1090 (tools/wave_model.cpp refill_min):
+    // MI355X A/B, config 4 at 2^24: +1.3 %
+    if (__popcll(freeb) < PXB_EV_REFILL_MIN && freeb != ~0ull) freeb = 0ull;
+#endif
     while (freeb != 0ull && !drained) {
       // (wave-uniform; a lane's sums only grow by instances it takes here)
       if (__builtin_amdgcn_ballot_w64(tot.c[0] >= EV_FLUSH) != 0ull) tot.flush(trow, lane);
@@ -172,8 +184,39 @@ __global__ __launch_bounds__(64, CMP ? 3 : SL ? 2 : 1) void paxos_ev_kernel(EvKP
       }
       const uint32_t take = min((uint32_t)__popcll(freeb), end - next);
       const uint32_t rank = (uint32_t)__popcll(freeb & below);
+      // Isolation windows of a launch-wide crash rate: the N draws of each
+      // instance taken are spread over the wave's lanes (one draw per lane for
+      // up to 64 / N instances) instead of N serial draws in the lanes that
+      // start one: a refill serves ~1 lane (a lane ends every ~17 wave-
+      // iterations), so the wave ran all N draws for it (config 4: ~300 of the
+      // ~600 instructions of a refill; tools/wave_model.cpp, tools/isa_budget.py)
+      uint32_t wpre[N] = {};
+#ifdef PXB_EV_COOP_WIN
+      const bool coop = (kp.p.cfg & (EV_CFG_CRASHY | EV_CFG_RANDOMIZE)) == EV_CFG_CRASHY;
+#else
+      const bool coop = false;            // (MI355X A/B, config 4: -0.3 %: not used)
+#endif
+      if (coop) {
+        const uint32_t nd = take * (uint32_t)N;
+        for (uint32_t base = 0; base < nd; base += 64u) {          // (wave-uniform)
+          const uint32_t d = base + lane;
+          const uint32_t r = d / (uint32_t)N, a = d - r * (uint32_t)N;
+          uint32_t wv = 0u;
+          if (d < nd) {
+            const uint64_t inst = kp.p.first_instance + (kp.n_ids ? kp.ids[next + r] : next + r);
+            const uint4 w = philox_rk((uint32_t)inst, (uint32_t)(inst >> 32), 0u, (3u << 24) | a, L.rk);
+            wv = decltype(L)::window_of(kp.p, w, kp.p.crash_m1);
+          }
+#pragma unroll
+          for (int q = 0; q < N; ++q) {
+            const uint32_t src = rank * (uint32_t)N + (uint32_t)q - base;   // (wraps below base)
+            const uint32_t v = (uint32_t)__shfl((int)wv, (int)(src & 63u), 64);
+            wpre[q] = (src < 64u) ? v : wpre[q];
+          }
+        }
+      }
+      if (((freeb >> lane) & 1ull) && rank < take) L.init(kp.p, kp.n_ids ? kp.ids[next + rank] : next + rank, coop ? wpre : nullptr);
       if (((freeb >> lane) & 1ull) && rank < take) {
-        L.init(kp.p, kp.n_ids ? kp.ids[next + rank] : next + rank);
         if (__builtin_expect(L.bailed, 0)) {   // (a fuzzed P above this shape's: the general kernel's)
           const uint32_t pos = atomicAdd(kp.bail_n, 1u);
           if (pos < kp.bail_cap) kp.bail_ids[pos] = L.gid;

@@ -29,15 +29,15 @@ struct HostMem {
   void orw(uint32_t i, uint32_t v) const { w[i] |= v; }
 };
 
-template <int PM, int N, int W, bool CMP, bool LG, bool SL>
+template <int PM, int N, int W, bool CMP, bool LG, bool SL, bool SP>
 int run_shape(const pxb_config* cfg, pxb_result* out, uint32_t* dig, pxb_acceptor_rec* acc, int64_t* tot,
               uint32_t* bail_ids, uint32_t* n_bail, uint64_t* micro_steps) {
   constexpr int POOL = EvPool<PM, N, CMP, LG, SL>::value;
-  using S = Shape<PM, N, POOL, W, CMP, LG, SL>;
+  using S = Shape<PM, N, POOL, W, CMP, LG, SL, SP>;
   g_words = S::WORDS;
   std::vector<uint32_t> buf(S::WORDS + 1, 0xDEADBEEFu);   // garbage: init must set what it reads
   const EvParams p = make_params(cfg);
-  EvLane<PM, N, POOL, W, CMP, HostMem, true, LG, SL> L;
+  EvLane<PM, N, POOL, W, CMP, HostMem, true, LG, SL, SP> L;
   L.m = HostMem{buf.data()};
   L.set_keys(p);
   uint32_t nb = 0;
@@ -91,29 +91,29 @@ int run_shape(const pxb_config* cfg, pxb_result* out, uint32_t* dig, pxb_accepto
   return 0;
 }
 
-template <int PM, int W, bool CMP, bool LG, bool SL>
+template <int PM, int W, bool CMP, bool LG, bool SL, bool SP>
 int run_n(const pxb_config* c, pxb_result* o, uint32_t* d, pxb_acceptor_rec* a, int64_t* t, uint32_t* b, uint32_t* nb,
           uint64_t* ms) {
   switch (c->n_acceptors) {
-    case 2: return run_shape<PM, 2, W, CMP, LG, SL>(c, o, d, a, t, b, nb, ms);
-    case 3: return run_shape<PM, 3, W, CMP, LG, SL>(c, o, d, a, t, b, nb, ms);
-    case 4: return run_shape<PM, 4, W, CMP, LG, SL>(c, o, d, a, t, b, nb, ms);
-    case 5: return run_shape<PM, 5, W, CMP, LG, SL>(c, o, d, a, t, b, nb, ms);
-    case 6: return run_shape<PM, 6, W, CMP, LG, SL>(c, o, d, a, t, b, nb, ms);
-    case 7: return run_shape<PM, 7, W, CMP, LG, SL>(c, o, d, a, t, b, nb, ms);
-    case 8: return run_shape<PM, 8, W, CMP, LG, SL>(c, o, d, a, t, b, nb, ms);
-    case 9: return run_shape<PM, 9, W, CMP, LG, SL>(c, o, d, a, t, b, nb, ms);
+    case 2: return run_shape<PM, 2, W, CMP, LG, SL, SP>(c, o, d, a, t, b, nb, ms);
+    case 3: return run_shape<PM, 3, W, CMP, LG, SL, SP>(c, o, d, a, t, b, nb, ms);
+    case 4: return run_shape<PM, 4, W, CMP, LG, SL, SP>(c, o, d, a, t, b, nb, ms);
+    case 5: return run_shape<PM, 5, W, CMP, LG, SL, SP>(c, o, d, a, t, b, nb, ms);
+    case 6: return run_shape<PM, 6, W, CMP, LG, SL, SP>(c, o, d, a, t, b, nb, ms);
+    case 7: return run_shape<PM, 7, W, CMP, LG, SL, SP>(c, o, d, a, t, b, nb, ms);
+    case 8: return run_shape<PM, 8, W, CMP, LG, SL, SP>(c, o, d, a, t, b, nb, ms);
+    case 9: return run_shape<PM, 9, W, CMP, LG, SL, SP>(c, o, d, a, t, b, nb, ms);
   }
   return -1;
 }
 
-template <int W, bool CMP, bool LG = false, bool SL = false>
+template <int W, bool CMP, bool LG = false, bool SL = false, bool SP = false>
 int run_w(const pxb_config* c, uint32_t pm, pxb_result* o, uint32_t* d, pxb_acceptor_rec* a, int64_t* t, uint32_t* b,
           uint32_t* nb, uint64_t* ms) {
   switch (pm) {
-    case 1: return run_n<1, W, CMP, LG, SL>(c, o, d, a, t, b, nb, ms);
-    case 2: return run_n<2, W, CMP, LG, SL>(c, o, d, a, t, b, nb, ms);
-    case 3: return run_n<3, W, CMP, LG, SL>(c, o, d, a, t, b, nb, ms);
+    case 1: return run_n<1, W, CMP, LG, SL, SP>(c, o, d, a, t, b, nb, ms);
+    case 2: return run_n<2, W, CMP, LG, SL, SP>(c, o, d, a, t, b, nb, ms);
+    case 3: return run_n<3, W, CMP, LG, SL, SP>(c, o, d, a, t, b, nb, ms);
   }
   return -1;
 }
@@ -126,7 +126,8 @@ extern "C" int ev_host_run(const pxb_config* cfg, pxb_result* out, uint32_t* dig
   const char* lv = getenv("EV_LAYOUT");                 // tests: force a layout
   const int layout = lv ? atoi(lv) : layout_for(cfg);
   if (layout == 2 && cfg->delay_max > 8) return -1;
-  if (layout == 3 && cfg->delay_max > 4) return -1;
+  if ((layout == 3 || layout == 6) && cfg->delay_max > 4) return -1;
+  if (layout == 6 && (cfg->loss_ppm || cfg->skew_max || (cfg->flags & PXB_CFG_RANDOMIZE) || cfg->n_ticks > 1)) return -1;
   if ((layout == 4) != (cfg->n_ticks > 1)) return -1;      // log mode runs on the log-mode fields only
   if ((layout == 0 || layout == 5) && cfg->delay_max > 8) return -1;
   // tests: the shape's proposer capacity; below n_proposers (fuzzed batches
@@ -145,6 +146,7 @@ extern "C" int ev_host_run(const pxb_config* cfg, pxb_result* out, uint32_t* dig
     case 3: return run_w<4, true>(cfg, pm, out, dig, acc, totals, bail_ids, n_bail, micro_steps);
     case 4: return run_w<8, false, true>(cfg, pm, out, dig, acc, totals, bail_ids, n_bail, micro_steps);
     case 5: return run_w<8, false, false, true>(cfg, pm, out, dig, acc, totals, bail_ids, n_bail, micro_steps);
+    case 6: return run_w<4, true, false, false, true>(cfg, pm, out, dig, acc, totals, bail_ids, n_bail, micro_steps);
   }
   return -1;
 }

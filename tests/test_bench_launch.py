@@ -28,17 +28,30 @@ def _bench(*args, env_extra=None):
 
 @pytest.mark.parametrize("gpus", [1, 2])
 def test_bench_launcher_ranks(gpus):
+    """The headline shape (BASELINE config 4, the north star): one batch per
+    step split over the ranks (strong scaling), totals all-reduced."""
     j = _bench("--dry-run", "--gpus", str(gpus), "--steps", "3", "--warmup", "1", "--instances", "500")
-    assert j["n_gpus"] == gpus and j["rccl_world"] == gpus
-    assert j["counters"]["instances"] == 500 * 3 * gpus     # all-reduced over the ranks
-    assert j["steps"] == 3 and j["ms_per_step"] > 0
-    # the north-star line: one fixed batch (the dry-run stand-in for 2^26)
-    # split over the ranks, strong scaling, totals all-reduced
-    ns = j["north_star"]
-    assert ns["n_gpus"] == gpus and ns["rccl_world"] == gpus and ns["scaling"] == "strong"
-    assert ns["instances_per_gpu_per_step"] * gpus == ns["instances_per_step"] == 1 << 12
-    assert ns["counters"]["instances"] == 1 << 12
-    assert ns["instances_per_s"] > 0
+    assert j["n_gpus"] == gpus and j["config"]["rccl_world"] == gpus and j["scaling"] == "strong"
+    assert j["config"]["instances_per_gpu_per_step"] * gpus == j["config"]["instances_per_step"] == 500 // gpus * gpus
+    assert j["counters"]["instances"] == 500 // gpus * gpus * 3     # all-reduced over the ranks
+    assert j["steps"] == 3 and j["ms_per_step"] > 0 and j["value"] > 0
+    assert "config 4 (north star)" in j["config"]["workload"]
+    # the default batch: the dry-run stand-in for 2^26
+    j = _bench("--dry-run", "--gpus", str(gpus), "--steps", "2", "--warmup", "0")
+    assert j["config"]["instances_per_step"] == 1 << 12 and j["counters"]["instances"] == 2 << 12
+
+
+def test_bench_defaults_to_north_star():
+    sys.path.insert(0, ROOT)
+    import bench
+    import argparse
+    old = sys.argv
+    sys.argv = ["bench.py"]
+    try:
+        a = bench.parse()
+    finally:
+        sys.argv = old
+    assert isinstance(a, argparse.Namespace) and a.config == 4 and a.gpus == 1
 
 
 def test_bench_rejects_world_mismatch():

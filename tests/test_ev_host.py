@@ -160,6 +160,24 @@ def test_config5_three_proposer_deep_response_fifos(monkeypatch):
     assert len(bails) > 0                            # (the pool and the rings still bail)
 
 
+@pytest.mark.parametrize("P", [1, 2, 3])
+@pytest.mark.parametrize("N", [2, 5, 7, 9])
+def test_simple_schedule_layout(P, N, monkeypatch):
+    """Layout 6 (compact, 4-step wheel, simple schedule: no loss, no Tick
+    skew, single decree; BASELINE config 4's routing): every proposer's Tick
+    is handled at init and the sends skip the loss test.  Exact against the
+    oracle on every topology, and the default routing picks it for config 4."""
+    cfg = pxb.Config(seed=0x51 + 16 * P + N, n_proposers=P, n_acceptors=N, delay_max=4,
+                     crash_ppm=250000, crash_len_max=12, crash_start_max=10, step_cap=300)
+    check(cfg, 99, 1200, max_bail_frac=0.5)
+    monkeypatch.setenv("EV_LAYOUT", "6")
+    check(pxb.CONFIGS[4], 777, 1000, max_bail_frac=0.03)
+    # a lossy or skewed batch is refused by the simple layout
+    monkeypatch.setenv("EV_LAYOUT", "6")
+    with pytest.raises(AssertionError):
+        ev_run(pxb.CONFIGS[3], 0, 10)
+
+
 @pytest.mark.parametrize("layout", [2, 3])
 @pytest.mark.parametrize("P", [1, 2, 3])
 @pytest.mark.parametrize("N", [2, 5, 9])
