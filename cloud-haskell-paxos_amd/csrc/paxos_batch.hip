@@ -279,13 +279,19 @@ constexpr uint32_t EV_BAIL_CAP = 1u << 22;
 constexpr uint64_t EV_SPLIT_CHUNK = 1ull << 25;
 constexpr uint32_t EV_SPLIT_CAP = (uint32_t)(EV_SPLIT_CHUNK / 2);
 // At most EV_LIST_STREAMS streams per device hold lists (created lazily, 16 MB
-// each + 64 MB for split routing); a further stream waits for the device and
-// takes over the oldest entry.
+// each + 64 MB for split routing).  An entry records an event behind the last
+// launches that use its lists; they are enqueued with g_mu held, so whoever
+// takes the entry over later (a stream beyond EV_LIST_STREAMS evicting the
+// oldest, or a new stream taking one that pxb_stream_release freed) first
+// waits for that event: two streams never share a list while either may
+// still run on it.
 constexpr int EV_LIST_STREAMS = 8;
 struct EvLists {
-  hipStream_t s;
+  hipStream_t s;                // owner (nullptr: free, buffers kept for the next owner)
   uint32_t* bail;
   uint32_t* split;
+  hipEvent_t ev;                // behind the owner's last launches on these lists
+  bool ev_set;
 };
 static EvLists g_lists[64][EV_LIST_STREAMS];
 static int g_nlists[64], g_lnext[64];
@@ -350,25 +356,47 @@ int pxb_debug_wave_times(unsigned long long* out, unsigned max_waves) {
 #endif
 int pxb_last_hip_error(void) { return g_last_hip; }
 
-// the bailed-id lists of (dev, stream) (callers hold g_mu)
-static int stream_lists(int dev, hipStream_t st, bool need_split, uint32_t** bail, uint32_t** split) {
+// the bailed-id lists of (dev, stream) (callers hold g_mu until their launches
+// on the lists are enqueued and list_used() has recorded the entry's event)
+static int stream_lists(int dev, hipStream_t st, bool need_split, uint32_t** bail, uint32_t** split,
+                        EvLists** ent) {
   EvLists* e = nullptr;
   for (int k = 0; k < g_nlists[dev] && !e; ++k)
     if (g_lists[dev][k].s == st) e = &g_lists[dev][k];
+  for (int k = 0; k < g_nlists[dev] && !e; ++k)      // a freed entry (its owner released it)
+    if (g_lists[dev][k].s == nullptr) e = &g_lists[dev][k];
   if (!e) {
-    if (g_nlists[dev] < EV_LIST_STREAMS) {
-      e = &g_lists[dev][g_nlists[dev]++];
-    } else {                                   // every entry taken: reuse one once the device is idle
-      HIPCHK(hipDeviceSynchronize());
-      e = &g_lists[dev][g_lnext[dev]++ % EV_LIST_STREAMS];
-    }
+    if (g_nlists[dev] < EV_LIST_STREAMS) e = &g_lists[dev][g_nlists[dev]++];
+    else e = &g_lists[dev][g_lnext[dev]++ % EV_LIST_STREAMS];   // every entry owned: take the oldest over
+  }
+  if (e->s != st) {                                  // new owner: the old one's launches must be done
+    if (e->ev_set) HIPCHK(hipEventSynchronize(e->ev));
     e->s = st;
   }
+  if (!e->ev) HIPCHK(hipEventCreateWithFlags(&e->ev, hipEventDisableTiming));
   if (!e->bail) HIPCHK(hipMalloc(&e->bail, (size_t)EV_BAIL_CAP * sizeof(uint32_t)));
   if (need_split && !e->split) HIPCHK(hipMalloc(&e->split, (size_t)EV_SPLIT_CAP * sizeof(uint32_t)));
   *bail = e->bail;
   *split = need_split ? e->split : nullptr;
+  *ent = e;
   return PXB_OK;
+}
+
+// after the launches that use an entry's lists are enqueued on its stream (g_mu held)
+static int list_used(EvLists* e, hipStream_t st) {
+  HIPCHK(hipEventRecord(e->ev, st));
+  e->ev_set = true;
+  return PXB_OK;
+}
+
+// A stream that is about to be destroyed gives up its lists (paxos_multi.cpp
+// creates a stream per device and call): the entry is freed for the next stream
+// (which waits for the event first), so lists never outlive their stream's use.
+extern "C" void pxb_stream_release(int dev, hipStream_t st) {
+  if (dev < 0 || dev >= 64 || !st) return;
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (int k = 0; k < g_nlists[dev]; ++k)
+    if (g_lists[dev][k].s == st) g_lists[dev][k].s = nullptr;
 }
 
 // per-device scratch of pxb_run_device (callers hold g_mu)
@@ -424,6 +452,7 @@ int pxb_shutdown(void) {
       for (int k = 0; k < g_nlists[d]; ++k) {
         if (g_lists[d][k].bail) (void)hipFree(g_lists[d][k].bail);
         if (g_lists[d][k].split) (void)hipFree(g_lists[d][k].split);
+        if (g_lists[d][k].ev) (void)hipEventDestroy(g_lists[d][k].ev);
         g_lists[d][k] = EvLists{};
       }
       g_nlists[d] = g_lnext[d] = 0;
@@ -628,14 +657,16 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
     kp.acc = d_acc ? reinterpret_cast<uint4*>(d_acc + done * cfg->n_acceptors) : nullptr;
     uint32_t *bail = nullptr, *slist = nullptr;
     unsigned long long* slot = nullptr;
+    EvLists* lent = nullptr;
+    // (held until this chunk's launches are enqueued: see EvLists)
+    std::unique_lock<std::mutex> lk(g_mu);
     {
-      std::lock_guard<std::mutex> lk(g_mu);
       const int sidx = (int)(g_qseq[dev]++ % QSLOTS);
       slot = g_slots[dev] + (size_t)sidx * SLOT_U64;
       kp.part = slot;
       kp.queue = reinterpret_cast<uint32_t*>(slot + 2 * ROWS_U64);
       if (use_ev || use_ff1 || use_ffp)
-        if (int rc2 = stream_lists(dev, st, split, &bail, &slist)) return rc2;
+        if (int rc2 = stream_lists(dev, st, split, &bail, &slist, &lent)) return rc2;
     }
     // a launch that fails after an earlier one of this chunk has queued leaves
     // the slot half used: zero it behind the queued work before reporting
@@ -760,6 +791,8 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
     hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(TCOPIES), 0, st, kp.part, kp.part + ROWS_U64, kp.queue,
                        bail_word, bail_cap, totals);
     if (hipError_t e = hipGetLastError()) return fail(e);
+    if (lent)
+      if (int rc2 = list_used(lent, st)) return rc2;
   }
   return PXB_OK;
 }

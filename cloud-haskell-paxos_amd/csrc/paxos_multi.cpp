@@ -79,6 +79,8 @@ bool injected(const char* phase, int g) {
   return p && d && strcmp(p, phase) == 0 && atoi(d) == g;
 }
 
+extern "C" void pxb_stream_release(int dev, hipStream_t st);   // paxos_batch.hip
+
 struct HipShards {
   const pxb_config* cfg;
   int G;
@@ -161,7 +163,10 @@ struct HipShards {
     if (d.d_dig) (void)hipFree(d.d_dig);
     if (d.d_acc) (void)hipFree(d.d_acc);
     if (d.d_tot) (void)hipFree(d.d_tot);
-    if (d.st) (void)hipStreamDestroy(d.st);
+    if (d.st) {
+      pxb_stream_release(g, d.st);      // (its bailed-id lists go back to the device's pool)
+      (void)hipStreamDestroy(d.st);
+    }
     d.st = nullptr;                  // (the fetched totals stay: they are the result)
     d.d_out = nullptr;
     d.d_dig = nullptr;

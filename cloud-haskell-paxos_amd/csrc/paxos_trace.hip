@@ -132,6 +132,10 @@ extern "C" int pxb_trace_instance(const pxb_config* cfg, uint64_t instance, pxb_
       cfg->n_acceptors > PXB_MAX_ACCEPTORS || cfg->delay_max < 1 || cfg->delay_max > PXB_MAX_DELAY ||
       cfg->step_cap < 1 || !eligible(cfg))
     return PXB_E_INVAL;
+  // single decree only: the trace kernel runs the single-decree fields (one
+  // Tick per proposer, 2-bit commands); eligible() admits log mode for the
+  // batch kernels' LG shape, so log mode is refused here explicitly
+  if (cfg->n_ticks > 1) return PXB_E_INVAL;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return PXB_E_NODEV;
   const bool prod = (cfg->flags & PXB_CFG_TRACE_PRODUCTION) != 0u;

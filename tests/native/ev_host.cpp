@@ -4,6 +4,7 @@
 // GPU.  The product runs the same EvLane code on the device
 // (paxos_ev_kernel.h); nothing here is linked into libpaxos_batch.so.
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -18,15 +19,42 @@ namespace {
 
 int g_words = 0;                                           // LDS words per lane of the last shape run
 
+// PXB_HOST_CHECKED (the sanitizer build, tests/test_ev_sanitized.py): every
+// access is checked against the shape's LDS words (S::WORDS), halfword
+// accesses against 2 * WORDS halfwords, before it is made
+#ifdef PXB_HOST_CHECKED
+#define PXB_HCHK(c)                                                                                   \
+  do {                                                                                              \
+    if (!(c)) {                                                                                     \
+      fprintf(stderr, "ev_host: LDS access out of the shape's words: %s (%s:%d)\n", #c, __FILE__, __LINE__); \
+      abort();                                                                                      \
+    }                                                                                               \
+  } while (0)
+#else
+#define PXB_HCHK(c) ((void)0)
+#endif
 struct HostMem {
   uint32_t* w;
-  uint32_t ld(uint32_t i) const { return w[i]; }
-  void st(uint32_t i, uint32_t v) const { w[i] = v; }
-  uint32_t ld16(uint32_t base, uint32_t i) const { return reinterpret_cast<const uint16_t*>(w + base)[i]; }
-  void st16(uint32_t base, uint32_t i, uint32_t v) const { reinterpret_cast<uint16_t*>(w + base)[i] = (uint16_t)v; }
-  uint32_t ld16h(uint32_t i, uint32_t half) const { return reinterpret_cast<const uint16_t*>(w + i)[half]; }
-  void st16h(uint32_t i, uint32_t half, uint32_t v) const { reinterpret_cast<uint16_t*>(w + i)[half] = (uint16_t)v; }
-  void orw(uint32_t i, uint32_t v) const { w[i] |= v; }
+  uint32_t n;                                              // the shape's words (S::WORDS)
+  uint32_t ld(uint32_t i) const { PXB_HCHK(i < n); return w[i]; }
+  void st(uint32_t i, uint32_t v) const { PXB_HCHK(i < n); w[i] = v; }
+  uint32_t ld16(uint32_t base, uint32_t i) const {
+    PXB_HCHK(2u * base + i < 2u * n);
+    return reinterpret_cast<const uint16_t*>(w + base)[i];
+  }
+  void st16(uint32_t base, uint32_t i, uint32_t v) const {
+    PXB_HCHK(2u * base + i < 2u * n);
+    reinterpret_cast<uint16_t*>(w + base)[i] = (uint16_t)v;
+  }
+  uint32_t ld16h(uint32_t i, uint32_t half) const {
+    PXB_HCHK(i < n && half < 2u);
+    return reinterpret_cast<const uint16_t*>(w + i)[half];
+  }
+  void st16h(uint32_t i, uint32_t half, uint32_t v) const {
+    PXB_HCHK(i < n && half < 2u);
+    reinterpret_cast<uint16_t*>(w + i)[half] = (uint16_t)v;
+  }
+  void orw(uint32_t i, uint32_t v) const { PXB_HCHK(i < n); w[i] |= v; }
 };
 
 template <int PM, int N, int W, bool CMP, bool LG, bool SL, bool SP>
@@ -35,10 +63,16 @@ int run_shape(const pxb_config* cfg, pxb_result* out, uint32_t* dig, pxb_accepto
   constexpr int POOL = EvPool<PM, N, CMP, LG, SL>::value;
   using S = Shape<PM, N, POOL, W, CMP, LG, SL, SP>;
   g_words = S::WORDS;
-  std::vector<uint32_t> buf(S::WORDS + 1, 0xDEADBEEFu);   // garbage: init must set what it reads
+  // garbage: init must set what it reads (checked builds: exactly WORDS, so
+  // ASan sees an access past them even where PXB_HCHK would not)
+#ifdef PXB_HOST_CHECKED
+  std::vector<uint32_t> buf(S::WORDS, 0xDEADBEEFu);
+#else
+  std::vector<uint32_t> buf(S::WORDS + 1, 0xDEADBEEFu);
+#endif
   const EvParams p = make_params(cfg);
   EvLane<PM, N, POOL, W, CMP, HostMem, true, LG, SL, SP> L;
-  L.m = HostMem{buf.data()};
+  L.m = HostMem{buf.data(), (uint32_t)S::WORDS};
   L.set_keys(p);
   uint32_t nb = 0;
   uint64_t ms = 0;
@@ -96,13 +130,15 @@ int run_n(const pxb_config* c, pxb_result* o, uint32_t* d, pxb_acceptor_rec* a, 
           uint64_t* ms) {
   switch (c->n_acceptors) {
     case 2: return run_shape<PM, 2, W, CMP, LG, SL, SP>(c, o, d, a, t, b, nb, ms);
+    case 5: return run_shape<PM, 5, W, CMP, LG, SL, SP>(c, o, d, a, t, b, nb, ms);
+    case 7: return run_shape<PM, 7, W, CMP, LG, SL, SP>(c, o, d, a, t, b, nb, ms);
+    case 9: return run_shape<PM, 9, W, CMP, LG, SL, SP>(c, o, d, a, t, b, nb, ms);
+#ifndef PXB_EV_HOST_FEW_N   // (the sanitizer build: the acceptor counts above only, half the compile time)
     case 3: return run_shape<PM, 3, W, CMP, LG, SL, SP>(c, o, d, a, t, b, nb, ms);
     case 4: return run_shape<PM, 4, W, CMP, LG, SL, SP>(c, o, d, a, t, b, nb, ms);
-    case 5: return run_shape<PM, 5, W, CMP, LG, SL, SP>(c, o, d, a, t, b, nb, ms);
     case 6: return run_shape<PM, 6, W, CMP, LG, SL, SP>(c, o, d, a, t, b, nb, ms);
-    case 7: return run_shape<PM, 7, W, CMP, LG, SL, SP>(c, o, d, a, t, b, nb, ms);
     case 8: return run_shape<PM, 8, W, CMP, LG, SL, SP>(c, o, d, a, t, b, nb, ms);
-    case 9: return run_shape<PM, 9, W, CMP, LG, SL, SP>(c, o, d, a, t, b, nb, ms);
+#endif
   }
   return -1;
 }
@@ -153,3 +189,43 @@ extern "C" int ev_host_run(const pxb_config* cfg, pxb_result* out, uint32_t* dig
 
 // the LDS words per lane of the shape the last ev_host_run used (tests: layout sizes)
 extern "C" int ev_host_last_words(void) { return g_words; }
+
+#ifdef PXB_EV_HOST_MAIN
+// Sanitizer-build driver (tests/test_ev_sanitized.py): one batch from the
+// command line, outputs to a file as raw little-endian words:
+//   rc, n, N, n_bail | results n x 4 | digests n x N | acceptor records n x N x 4
+//   | totals 16 x int64 | bailed ids n_bail
+// argv: out seed first n P N loss delay crash clen cstart skew cap flags ticks period
+int main(int argc, char** argv) {
+  if (argc != 17) {
+    fprintf(stderr, "usage: %s out seed first n P N loss delay crash clen cstart skew cap flags ticks period\n", argv[0]);
+    return 2;
+  }
+  pxb_config c{};
+  c.seed = strtoull(argv[2], nullptr, 0);
+  c.first_instance = strtoull(argv[3], nullptr, 0);
+  c.n_instances = strtoull(argv[4], nullptr, 0);
+  uint32_t* f[] = {&c.n_proposers, &c.n_acceptors, &c.loss_ppm, &c.delay_max, &c.crash_ppm, &c.crash_len_max,
+                   &c.crash_start_max, &c.skew_max, &c.step_cap, &c.flags, &c.n_ticks, &c.tick_period};
+  for (int i = 0; i < 12; ++i) *f[i] = (uint32_t)strtoul(argv[5 + i], nullptr, 0);
+  const uint64_t n = c.n_instances, N = c.n_acceptors;
+  std::vector<pxb_result> res(n);
+  std::vector<uint32_t> dig(n * N), bails(n + 1);
+  std::vector<pxb_acceptor_rec> acc(n * N);
+  int64_t tot[16] = {0};
+  uint32_t nb = 0;
+  uint64_t ms = 0;
+  const int rc = ev_host_run(&c, res.data(), dig.data(), acc.data(), tot, bails.data(), &nb, &ms);
+  FILE* o = fopen(argv[1], "wb");
+  if (!o) return 3;
+  const uint32_t hdr[4] = {(uint32_t)rc, (uint32_t)n, (uint32_t)N, nb};
+  fwrite(hdr, 4, 4, o);
+  fwrite(res.data(), sizeof(pxb_result), n, o);
+  fwrite(dig.data(), 4, n * N, o);
+  fwrite(acc.data(), sizeof(pxb_acceptor_rec), n * N, o);
+  fwrite(tot, 8, 16, o);
+  fwrite(bails.data(), 4, nb, o);
+  fclose(o);
+  return rc == 0 ? 0 : 4;
+}
+#endif

@@ -74,6 +74,23 @@ def test_invalid_config_rejected():
     assert lib.pxb_run_device(C.byref(bad), None, None, None, C.cast(tot, C.c_void_p), None) == pxb.PXB_E_INVAL
 
 
+def test_trace_refuses_log_mode():
+    """pxb_trace_instance runs the single-decree fields only: a log-mode config
+    (n_ticks > 1, which the batch kernels' LG shape admits) is PXB_E_INVAL,
+    checked before any device call (so on every host, GPU or not)."""
+    import numpy as np
+    lib = pxb.load()
+    buf = np.zeros((16, pxb.TRACE_WORDS), dtype=np.uint32)
+    n = C.c_uint32(0)
+    res = np.zeros(4, dtype=np.uint32)
+    for cfg in (pxb.LOG_CONFIG, pxb.LOG_FAULTY_CONFIG):
+        c = cfg.to_c(0, 1)
+        assert lib.pxb_trace_instance(C.byref(c), 0, C.c_void_p(buf.ctypes.data), 16, C.byref(n),
+                                      C.c_void_p(res.ctypes.data)) == pxb.PXB_E_INVAL
+        with pytest.raises(pxb.PaxosError, match="invalid argument"):
+            pxb.trace_instance(cfg, 0, max_records=16)
+
+
 def test_no_cpu_fallback_without_gpu():
     import torch
     if torch.cuda.is_available():

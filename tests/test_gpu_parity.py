@@ -469,6 +469,80 @@ def test_run_multi_matches_single_device(gpu_lib):
     assert np.array_equal(res, eres) and np.array_equal(dig, edig) and cnt == ecnt
 
 
+def test_many_streams_concurrent(gpu_lib):
+    """More concurrent streams than a device keeps bailed-id lists for (8):
+    12 host threads, each on its own HIP stream, run config 4 (which bails
+    ~0.5 % of its instances to a per-stream list) at once, twice over.  An
+    evicted list is only handed to a new stream after the old owner's launches
+    on it are done, so every thread's results and totals equal its own
+    single-stream run."""
+    import threading
+    import torch
+    cfg = pxb.CONFIGS[4]
+    n, T = 20000, 12
+    want = [pxb.run(cfg, 100000 * t, n) for t in range(T)]
+    got = [None] * T
+    errs = []
+
+    def worker(t):
+        try:
+            st = torch.cuda.Stream()
+            out = torch.zeros((n, 4), dtype=torch.int32, device="cuda")
+            dig = torch.zeros((n, cfg.n_acceptors), dtype=torch.int32, device="cuda")
+            tot = torch.zeros(16, dtype=torch.int64, device="cuda")
+            for _ in range(2):
+                tot.zero_()
+                with torch.cuda.stream(st):
+                    pxb.run_device(cfg, 100000 * t, n, d_results=out, d_digests=dig, d_totals=tot,
+                                   stream=st.cuda_stream)
+                st.synchronize()
+            got[t] = (out.cpu().numpy().view(np.uint32), dig.cpu().numpy().view(np.uint32),
+                      pxb.counters_dict(tot.cpu().tolist()))
+        except Exception as e:   # (reported by the main thread)
+            errs.append(e)
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(T)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errs, errs
+    for t in range(T):
+        assert np.array_equal(got[t][0], want[t][0]) and np.array_equal(got[t][1], want[t][1])
+        assert got[t][2] == want[t][3]
+
+
+def test_run_multi_repeated_calls_release_stream_lists(gpu_lib):
+    """pxb_run_multi makes a stream per device and call and gives its lists
+    back when it tears the stream down: 12 calls in a row (more than the 8
+    list entries of a device) stay exact."""
+    cfg = pxb.CONFIGS[4]
+    want = pxb.run(cfg, 5, 8000)
+    for _ in range(12):
+        res, dig, cnt = pxb.run_multi(cfg, 5, 8000)
+        assert np.array_equal(res, want[0]) and np.array_equal(dig, want[1]) and cnt == want[3]
+
+
+def test_config5_full_sweep_totals(gpu_lib):
+    """BASELINE config 5 at its stated size: all 2^28 randomized schedules on
+    one GPU in one call (run totals only, no per-instance outputs).  The
+    totals equal the sum of the eight 2^25 per-GPU shares run separately (the
+    8-GPU sharding), and every schedule is counted decided or undecided."""
+    import torch
+    cfg = pxb.CONFIGS[5]
+    n = pxb.CONFIG_INSTANCES[5]
+    tot = torch.zeros(16, dtype=torch.int64, device="cuda")
+    pxb.run_device(cfg, 0, n, d_totals=tot)
+    torch.cuda.synchronize()
+    full = pxb.counters_dict(tot.cpu().tolist())
+    assert full["instances"] == n and full["decided"] + full["undecided"] == n
+    shares = torch.zeros(16, dtype=torch.int64, device="cuda")
+    for k in range(8):
+        pxb.run_device(cfg, k * (n // 8), n // 8, d_totals=shares)
+    torch.cuda.synchronize()
+    assert pxb.counters_dict(shares.cpu().tolist()) == full
+
+
 @pytest.mark.parametrize("phase", ["setup", "compute"])
 def test_run_multi_shard_failure_returns_promptly(gpu_lib, phase):
     """A device that fails before the collective makes pxb_run_multi return its
