@@ -78,9 +78,16 @@ struct Shape {
   static constexpr int WW = (NLQ + NIN <= 32) ? 1 : 2;   // wheel words per slot
   static constexpr int ISH = (WW == 1) ? NLQ : 0;    // input-bit offset in its wheel word
   static constexpr int IB = POOL <= 32 ? 5 : 6;      // pool index bits
-  // request FIFO: QC entries of 7 bits, length at QL (QLB bits); compact: the
-  // reply seq of the same (a, p) pair in the word's top KB bits
-  static constexpr int QC = CMP ? 3 : 4, QL = 7 * QC, QLB = CMP ? 2 : 3;
+  // request FIFO: QC entries of EB bits (ring slot SB bits, due mod 2^DB), length
+  // at QL (QLB bits); compact: the reply seq of the same (a, p) pair in the
+  // word's top KB bits.  Compact on the 4-step wheel (delays <= 4): 5-bit
+  // entries (4 ring slots: 2 bits; every queued due lies in [sb, sb + 5]: due
+  // mod 8), so 4 of them fit beside a 9-bit reply seq (3-entry FIFOs bailed
+  // 0.46 % of config 4's instances, 98 % of them on a full request FIFO;
+  // tools/wave_model.cpp)
+  static constexpr bool C5 = CMP && W == 4;
+  static constexpr int EB = C5 ? 5 : 7, SB = C5 ? 2 : 3, DB = EB - SB;
+  static constexpr int QC = (CMP && !C5) ? 3 : 4, QL = EB * QC, QLB = (QC == 4) ? 3 : 2;
   static constexpr int KSH = QL + QLB, KB = 32 - KSH;
   // response FIFO: RC pool indices of IB bits, length at RL (RLB bits), tail due at RD;
   // slim over > 18 links (RSN): RC = 5 entries, each its pool index + 1 (0: empty),
@@ -129,8 +136,10 @@ struct Shape {
 // Layouts (docs/SEMANTICS.md §2 encodings; tickets < 2^12):
 //   request-link word   entry i (7 bits at 7i): broadcast slot [2:0] | due&15 [6:3]; len at QL
 //                       (compact: 3 entries, len [22:21], and the reply seq of the same
-//                       (a, p) pair in [31:23], one word for both; else 4 entries, len
-//                       [30:28], reply seq in its own halfword)
+//                       (a, p) pair in [31:23], one word for both; compact on the 4-step
+//                       wheel: 4 entries of 5 bits, slot [1:0] | due&7 [4:2], len [22:20],
+//                       reply seq [31:23]; else 4 entries, len [30:28], reply seq in its
+//                       own halfword)
 //   response-link word  pool index i (IB bits at IB*i); len [4IB+2:4IB]; last due&15 above it
 //                       (compact, pool <= 24: index 24 + (due & 7) = a Round2Success, no
 //                       pool word; dues stay within s + delay_max <= s + 4;
@@ -191,6 +200,10 @@ __host__ __device__ __forceinline__ bool any_lane(bool p) {
 enum : uint32_t {
   EVP_END = 1u << 0, EVP_FIN = 1u << 1, EVP_RUN = 1u << 2, EVP_TICK_ENTER = 1u << 3, EVP_TICK_END = 1u << 4,
   EVP_ACC = 1u << 5, EVP_PROP = 1u << 6, EVP_COPY = 1u << 7, EVP_SEND1 = 1u << 8, EVP_BCAST = 1u << 9,
+  // bail causes: ring slot still referenced, response FIFO full, response pool
+  // empty, request FIFO full, log length, reply seq
+  EVB_RING = 1u << 16, EVB_RFIFO = 1u << 17, EVB_POOL = 1u << 18, EVB_QFIFO = 1u << 19, EVB_LOG = 1u << 20,
+  EVB_RSEQ = 1u << 21,
 };
 #if defined(PXB_EV_PROBES) && !defined(__HIP_DEVICE_COMPILE__)
 extern thread_local uint32_t ev_probe_bits;
@@ -224,6 +237,7 @@ struct EvLane {
   static constexpr uint32_t WM = (uint32_t)W - 1u;
   static constexpr uint32_t QLM = (1u << S::QLB) - 1u, RLM = (1u << S::RLB) - 1u;
   static constexpr uint32_t IM = (1u << S::IB) - 1u;
+  static constexpr uint32_t DM = (1u << S::DB) - 1u;     // request-entry due mask
 
   Mem m;
   uint32_t rk[20];                    // Philox round keys (set_keys): uniform, held in VGPRs
@@ -557,6 +571,7 @@ struct EvLane {
     // a ring slot still referenced by a queued copy
     // (non-short-circuit: || here became two exec-mask branches)
     bailed = bailed | (p0 & (((rc >> (4u * slot0)) & 15u) != 0u)) | (p1 & (((rc >> (4u * slot1)) & 15u) != 0u));
+    PXB_EV_PROBE(EVB_RING, (p0 & (((rc >> (4u * slot0)) & 15u) != 0u)) | (p1 & (((rc >> (4u * slot1)) & 15u) != 0u)));
     PXB_EV_PROBE(EVP_BCAST, p0);
     if (p0) {                                        // (p1 only with p0)
       if constexpr (LG) {
@@ -627,13 +642,17 @@ struct EvLane {
       rtail = (wv >> S::RD) & 15u;
     }
     const uint32_t len = isR ? rlen : (wv >> S::QL) & QLM;
-    const uint32_t tail = isR ? rtail : (wv >> ((7u * len - 4u) & 31u)) & 15u;
-    const uint32_t rel = (tail - b4) & (len ? 15u : 0u);
+    // (a request entry's due is mod 2^DB: every queued due lies within 2^DB of the send step)
+    const uint32_t tail = isR ? rtail : (wv >> (((uint32_t)S::EB * len - (uint32_t)S::DB) & 31u)) & DM;
+    const uint32_t rel = (tail - b4) & (len ? (isR ? 15u : DM) : 0u);
     const uint32_t due_rel = d > rel ? d : rel;
     const uint32_t due4 = (b4 + due_rel) & 15u;
     // (a Round2Success in a compact link word needs no pool word)
     const bool r2c = S::RCODE & isR & ((rp.pw >> 30) == R2S);
     bailed = bailed | (go & (isR ? (len >= (uint32_t)S::RC) | ((pfree == 0) & !r2c) : (len >= (uint32_t)S::QC)));
+    PXB_EV_PROBE(EVB_RFIFO, go & isR & (len >= (uint32_t)S::RC));
+    PXB_EV_PROBE(EVB_POOL, go & isR & (pfree == 0) & !r2c);
+    PXB_EV_PROBE(EVB_QFIFO, go & !isR & (len >= (uint32_t)S::QC));
     const uint32_t k2 = (POOL > 32) ? (uint32_t)__builtin_ctzll((unsigned long long)pfree | (1ull << 63))
                                     : ctz32((uint32_t)pfree) & 31u;
     // the pool word: to a free entry (harmless unless a reply goes), or, with
@@ -649,7 +668,7 @@ struct EvLane {
     constexpr int RD = S::RSN ? 0 : S::RD;          // (no due field in a slim >18-link word)
     const uint32_t nR = S::RSN ? wv | (ent << ((S::IB * len) & 31u))
                                : ((wv + (1u << S::RL) + (ent << (S::IB * len))) & ~(15u << RD)) | (due4 << RD);
-    const uint32_t nQ = wv + (1u << S::QL) + ((cslot | (due4 << 3)) << (7u * len));
+    const uint32_t nQ = wv + (1u << S::QL) + ((cslot | ((due4 & DM) << S::SB)) << ((uint32_t)S::EB * len));
     m.st(lw, go ? (isR ? nR : nQ) : wv);
     put(refc, cp, get(refc, cp) + ((go & !isR) ? 1u << (4u * cslot) : 0u));
     // a carried copy due now joins this step's due links, the rest the wheel
@@ -693,12 +712,13 @@ struct EvLane {
     const uint32_t wq = m.ld(S::REQ + Lq);
     const uint32_t qlen = (wq >> S::QL) & QLM;
     bailed = bailed | (go & (qlen >= (uint32_t)S::QC));
-    const uint32_t rel = (((wq >> ((7u * qlen - 4u) & 31u)) & 15u) - s4) & (qlen ? 15u : 0u);   // tail's due - sb
+    PXB_EV_PROBE(EVB_QFIFO, go & (qlen >= (uint32_t)S::QC));
+    const uint32_t rel = (((wq >> (((uint32_t)S::EB * qlen - (uint32_t)S::DB) & 31u)) & DM) - s4) & (qlen ? DM : 0u);   // tail's due - sb
     const uint32_t due_rel = d > rel ? d : rel;
-    const uint32_t ent = cslot | (((s4 + due_rel) & 15u) << 3);
+    const uint32_t ent = cslot | (((s4 + due_rel) & DM) << S::SB);
     // (inactive lanes store their word back unchanged)
     // (entries above the length are 0: a pop shifts zeros in; a full FIFO bails)
-    m.st(S::REQ + Lq, go ? wq + (1u << S::QL) + (ent << (7u * qlen)) : wq);
+    m.st(S::REQ + Lq, go ? wq + (1u << S::QL) + (ent << ((uint32_t)S::EB * qlen)) : wq);
     put(refc, cp, get(refc, cp) + (go ? 1u << (4u * cslot) : 0u));
     // due at s (a carried-over copy with the shortest delay): straight into
     // this step's due links, else into the wheel
@@ -757,11 +777,11 @@ struct EvLane {
     const uint32_t kw = SL ? get(rseqv, L >> 2) : 0u;
     const uint32_t kr = S::CMP ? (wq >> S::KSH) : SL ? (kw >> (8u * (L & 3u))) & 0xFFu : m.ld16(S::RSEQ, L);
     const uint32_t len = (wq >> S::QL) & QLM;
-    const uint32_t bslot = wq & 7u;
+    const uint32_t bslot = wq & ((1u << S::SB) - 1u);
     // the popped word: entries shifted down one, length - 1 (fields above the
     // entries, length and reply seq, adjusted in place)
-    const uint32_t rq2 = ((wq & ((1u << S::QL) - 1u)) >> 7) + ((wq & ~((1u << S::QL) - 1u)) - (1u << S::QL));
-    const bool keep = (len > 1u) & (((wq >> 10) & 15u) == s4);   // the next entry due now too
+    const uint32_t rq2 = ((wq & ((1u << S::QL) - 1u)) >> S::EB) + ((wq & ~((1u << S::QL) - 1u)) - (1u << S::QL));
+    const bool keep = (len > 1u) & (((wq >> (S::EB + S::SB)) & DM) == (s4 & DM));   // the next entry due now too
     acc_mask = (acc & !keep) ? (acc_mask & ~(1u << L)) : acc_mask;
     uint32_t kind, x, z;
     if constexpr (LG) {
@@ -800,6 +820,7 @@ struct EvLane {
     PXB_EV_PROBE(EVP_RUN, run);
     if (__builtin_expect(run, 0)) {                  // executed <>= [c]: log, digest, divergence
       if (log_len >= A_LEN_MAX) bailed = true;
+      PXB_EV_PROBE(EVB_LOG, log_len >= A_LEN_MAX);
       put(accd, a, fnv_u32(get(accd, a), code_of(val)));
       if constexpr (LG) {                            // the canonical log's first LOG_TRACK positions (LDS)
         if (log_len < (uint32_t)PXB_LOG_TRACK) {
@@ -841,6 +862,7 @@ struct EvLane {
     const uint4 w1 = draw(snd1 ? kr : cc.x, snd1 ? (1u << 24) | (1u << 16) | (p << 8) | a : cc.y);
     msgs += snd1 ? 1u : 0u;
     bailed = bailed | (snd1 & (kr == (S::CMP ? (1u << S::KB) - 1u : SL ? 0xFFu : 0xFFFFu)));
+    PXB_EV_PROBE(EVB_RSEQ, snd1 & (kr == (S::CMP ? (1u << S::KB) - 1u : SL ? 0xFFu : 0xFFFFu)));
     if constexpr (SL) put(rseqv, L >> 2, kw + (snd1 ? 1u << (8u * (L & 3u)) : 0u));
     else if constexpr (!S::CMP) m.st16(S::RSEQ, L, snd1 ? kr + 1u : kr);
     rp.snd = snd1;

@@ -56,6 +56,7 @@ void model(const pxb_config* cfg, uint32_t n, uint32_t refill_min) {
   }
   uint64_t wave_it = 0, live_lane_it = 0, any[NB] = {}, sum[NB] = {};
   uint64_t refills = 0, inits = 0, out_its = 0, outs = 0, bails = 0, bail_its = 0, done_inst = 0;
+  uint64_t bcause[6] = {};
   uint32_t next = 0;
   for (;;) {
     // refill (the kernel: every idle lane, from the wave's chunk of the queue)
@@ -92,6 +93,7 @@ void model(const pxb_config* cfg, uint32_t n, uint32_t refill_min) {
       orb |= ev_probe_bits;
       for (int b = 0; b < NB; ++b) sum[b] += (ev_probe_bits >> b) & 1u;
       if (L[l].bailed) {
+        for (int b = 0; b < 6; ++b) bcause[b] += (ev_probe_bits >> (16 + b)) & 1u;
         L[l].mode = M_IDLE;
         L[l].bailed = false;
         ++bails;
@@ -113,6 +115,10 @@ void model(const pxb_config* cfg, uint32_t n, uint32_t refill_min) {
          64.0 * wave_it / I, live_lane_it / I, (double)live_lane_it / wave_it);
   printf("refills per instance (wave-level) %.4f, lanes per refill %.2f; output blocks per instance %.4f\n",
          refills / I, (double)inits / refills, out_its / I);
+  printf("bail causes (an instance may have several): ring %llu, response FIFO %llu, pool %llu, request FIFO %llu, "
+         "log %llu, reply seq %llu\n", (unsigned long long)bcause[0], (unsigned long long)bcause[1],
+         (unsigned long long)bcause[2], (unsigned long long)bcause[3], (unsigned long long)bcause[4],
+         (unsigned long long)bcause[5]);
   printf("%-11s %10s %10s\n", "region", "wave-frac", "lane-frac");
   for (int b = 0; b < NB; ++b)
     printf("%-11s %10.4f %10.4f\n", names[b], (double)any[b] / wave_it, (double)sum[b] / live_lane_it);
