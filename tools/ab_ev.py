@@ -43,7 +43,7 @@ def main():
         row = []
         for c, n, reps in CASES:
             ms, t = timeit(pxb.CONFIGS[c], n, reps)
-            ok = ref.setdefault(c, t) == t
+            ok = ref.setdefault((c, n), t) == t
             row.append("c%d %8.2f ms %6.1f M/s%s" % (c, ms, n / ms / 1e3, "" if ok else " TOTALS DIFFER"))
         print("%-26s %s" % (os.path.basename(lib), " | ".join(row)), flush=True)
 
