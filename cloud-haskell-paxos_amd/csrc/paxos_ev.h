@@ -605,11 +605,12 @@ struct EvLane {
   // The iteration's first send, on draw w: the acceptor's reply on link
   // a -> p (response FIFO + pool word) when there is one, else the next copy
   // of the oldest pending broadcast (request FIFO); one code path for both.
-  __host__ __device__ __forceinline__ void send_first(const EvParams& kp, const uint4& w, const Reply& rp) {
-    const bool isR = rp.snd;
+  __host__ __device__ __forceinline__ void send_first(const EvParams& kp, const uint4& w, const Reply& rp,
+                                                     bool act = true) {
+    const bool isR = rp.snd;                         // (only with act: acc_op)
     // the copy's bookkeeping (as in copy_send)
     const uint32_t sb = (uint32_t)s - (pq_old ? 1u : 0u);
-    const bool csnd = !isR & (pq_len != 0u);
+    const bool csnd = act & !isR & (pq_len != 0u);
     const uint32_t ce = pq & 31u;
     const uint32_t cp = ce >> 3, cslot = ce & 7u, ca = acur;
     const uint32_t ck = get(nsent, cp);
@@ -735,7 +736,9 @@ struct EvLane {
   // copy's, and the reply's or else the second copy's (1.4 of the 3 sends an
   // iteration can make are used on average; that copy's counter is known
   // before the acceptor part, which does not touch the pending queue).
-  __host__ __device__ __forceinline__ bool step(const EvParams& kp, EvOut& o) {
+  // (act = false: an idle lane of the wave, every op predicated off: the
+  // driver runs the iteration without an exec-mask branch around it)
+  __host__ __device__ __forceinline__ bool step(const EvParams& kp, EvOut& o, bool act = true) {
     // The proposer input first, so its link and pool loads start the
     // iteration instead of waiting behind the acceptor op; a pop and an append
     // on one FIFO commute (bails may differ, and stay exact).  MI355X, 2^24
@@ -744,15 +747,15 @@ struct EvLane {
     // overlaps the acceptor op (config 4 +1.7 %, config 3 +0.7 %, config 5 +0.9 %);
     // the copy before the proposer op measured 1-3 % slower.
     Reply rp;
-    prop_op(kp, true);
+    prop_op(kp, act);
     const uint2 c = copy_ctr();
-    copy_send(kp, true, draw(c.x, c.y));
+    copy_send(kp, act, draw(c.x, c.y));
     // (taking the acceptor op's choice before the copy is exact too, and
     // measured 1.5-2.5 % slower)
     const uint32_t ready = acc_ready_mask();
-    const uint4 w0 = acc_op(kp, true, copy_ctr(), rp, ready);
-    send_first(kp, w0, rp);
-    return end_op(kp, o, true);
+    const uint4 w0 = acc_op(kp, act, copy_ctr(), rp, ready);
+    send_first(kp, w0, rp, act);
+    return end_op(kp, o, act);
   }
 
   // ================= ACC: one due request (Server.hs:51-78) and its reply =================

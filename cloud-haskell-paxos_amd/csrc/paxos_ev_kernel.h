@@ -153,92 +153,98 @@ __global__ __launch_bounds__(64, CMP ? 3 : SL ? 2 : 1) void paxos_ev_kernel(EvKP
   uint32_t next = 0, end = 0;
   bool drained = false;
 
-  for (;;) {
-    // ---- refill idle lanes from the wave's chunk of the queue ----
-    uint64_t freeb = __builtin_amdgcn_ballot_w64(L.mode == M_IDLE);
 #ifndef PXB_EV_REFILL_MIN
 #define PXB_EV_REFILL_MIN 2
 #endif
-#if PXB_EV_REFILL_MIN > 1
-    // A refill runs only once two lanes are idle (or none is live): a refill
-    // costs the wave ~600 instructions whether it starts one lane or several,
-    // and a lane ends every ~17 wave-iterations (config 4), so nearly every
-    // refill started one lane.  Waiting for a second costs each instance ~8
-    // idle lane-iterations of its ~1090 (tools/wave_model.cpp refill_min):
-    // MI355X A/B, config 4 at 2^24: +1.3 %
-    if (__popcll(freeb) < PXB_EV_REFILL_MIN && freeb != ~0ull) freeb = 0ull;
-#endif
-    while (freeb != 0ull && !drained) {
-      // (wave-uniform; a lane's sums only grow by instances it takes here)
-      if (__builtin_amdgcn_ballot_w64(tot.c[0] >= EV_FLUSH) != 0ull) tot.flush(trow, lane);
-      if (next >= end) {
-        uint32_t c = 0;
-        if (lane == 0) c = atomicAdd(kp.queue, EV_QCHUNK);
-        c = (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
-        if (c >= n) {
-          drained = true;
-          break;
-        }
-        next = c;
-        end = min(c + EV_QCHUNK, n);
-      }
-      const uint32_t take = min((uint32_t)__popcll(freeb), end - next);
-      const uint32_t rank = (uint32_t)__popcll(freeb & below);
-      // Isolation windows of a launch-wide crash rate: the N draws of each
-      // instance taken are spread over the wave's lanes (one draw per lane for
-      // up to 64 / N instances) instead of N serial draws in the lanes that
-      // start one: a refill serves ~1 lane (a lane ends every ~17 wave-
-      // iterations), so the wave ran all N draws for it (config 4: ~300 of the
-      // ~600 instructions of a refill; tools/wave_model.cpp, tools/isa_budget.py)
-      uint32_t wpre[N] = {};
-#ifdef PXB_EV_COOP_WIN
-      const bool coop = (kp.p.cfg & (EV_CFG_CRASHY | EV_CFG_RANDOMIZE)) == EV_CFG_CRASHY;
-#else
-      const bool coop = false;            // (MI355X A/B, config 4: -0.3 %: not used)
-#endif
-      if (coop) {
-        const uint32_t nd = take * (uint32_t)N;
-        for (uint32_t base = 0; base < nd; base += 64u) {          // (wave-uniform)
-          const uint32_t d = base + lane;
-          const uint32_t r = d / (uint32_t)N, a = d - r * (uint32_t)N;
-          uint32_t wv = 0u;
-          if (d < nd) {
-            const uint64_t inst = kp.p.first_instance + (kp.n_ids ? kp.ids[next + r] : next + r);
-            const uint4 w = philox_rk((uint32_t)inst, (uint32_t)(inst >> 32), 0u, (3u << 24) | a, L.rk);
-            wv = decltype(L)::window_of(kp.p, w, kp.p.crash_m1);
+  // Idle lanes of the wave (wave-uniform, kept in a scalar): the refill below
+  // runs only once it can start PXB_EV_REFILL_MIN lanes, or when no lane is
+  // live, and the count is only re-taken after a lane ended or bailed.  A
+  // refill costs the wave ~600 instructions whether it starts one lane or
+  // several, and a lane ends every ~17 wave-iterations (config 4), so nearly
+  // every refill started one lane; waiting for a second costs each instance
+  // ~8 idle lane-iterations of its ~1090 (tools/wave_model.cpp refill_min):
+  // MI355X A/B, config 4 at 2^24: +1.3 %.  Idle lanes run the iteration with
+  // every op predicated off (step(..., act = false)), so no exec-mask branch
+  // surrounds it, and the per-iteration refill test is one scalar compare.
+  uint32_t nidle = 64u;
+  for (;;) {
+    if (nidle == 64u || (nidle >= (uint32_t)PXB_EV_REFILL_MIN && !drained)) {
+      // ---- refill idle lanes from the wave's chunk of the queue ----
+      uint64_t freeb = __builtin_amdgcn_ballot_w64(L.mode == M_IDLE);
+      while (freeb != 0ull && !drained) {
+        // (wave-uniform; a lane's sums only grow by instances it takes here)
+        if (__builtin_amdgcn_ballot_w64(tot.c[0] >= EV_FLUSH) != 0ull) tot.flush(trow, lane);
+        if (next >= end) {
+          uint32_t c = 0;
+          if (lane == 0) c = atomicAdd(kp.queue, EV_QCHUNK);
+          c = (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
+          if (c >= n) {
+            drained = true;
+            break;
           }
-#pragma unroll
-          for (int q = 0; q < N; ++q) {
-            const uint32_t src = rank * (uint32_t)N + (uint32_t)q - base;   // (wraps below base)
-            const uint32_t v = (uint32_t)__shfl((int)wv, (int)(src & 63u), 64);
-            wpre[q] = (src < 64u) ? v : wpre[q];
+          next = c;
+          end = min(c + EV_QCHUNK, n);
+        }
+        const uint32_t take = min((uint32_t)__popcll(freeb), end - next);
+        const uint32_t rank = (uint32_t)__popcll(freeb & below);
+        // Isolation windows of a launch-wide crash rate: the N draws of each
+        // instance taken are spread over the wave's lanes (one draw per lane for
+        // up to 64 / N instances) instead of N serial draws in the lanes that
+        // start one: a refill serves ~1 lane (a lane ends every ~17 wave-
+        // iterations), so the wave ran all N draws for it (config 4: ~300 of the
+        // ~600 instructions of a refill; tools/wave_model.cpp, tools/isa_budget.py)
+        uint32_t wpre[N] = {};
+  #ifdef PXB_EV_COOP_WIN
+        const bool coop = (kp.p.cfg & (EV_CFG_CRASHY | EV_CFG_RANDOMIZE)) == EV_CFG_CRASHY;
+  #else
+        const bool coop = false;            // (MI355X A/B, config 4: -0.3 %: not used)
+  #endif
+        if (coop) {
+          const uint32_t nd = take * (uint32_t)N;
+          for (uint32_t base = 0; base < nd; base += 64u) {          // (wave-uniform)
+            const uint32_t d = base + lane;
+            const uint32_t r = d / (uint32_t)N, a = d - r * (uint32_t)N;
+            uint32_t wv = 0u;
+            if (d < nd) {
+              const uint64_t inst = kp.p.first_instance + (kp.n_ids ? kp.ids[next + r] : next + r);
+              const uint4 w = philox_rk((uint32_t)inst, (uint32_t)(inst >> 32), 0u, (3u << 24) | a, L.rk);
+              wv = decltype(L)::window_of(kp.p, w, kp.p.crash_m1);
+            }
+  #pragma unroll
+            for (int q = 0; q < N; ++q) {
+              const uint32_t src = rank * (uint32_t)N + (uint32_t)q - base;   // (wraps below base)
+              const uint32_t v = (uint32_t)__shfl((int)wv, (int)(src & 63u), 64);
+              wpre[q] = (src < 64u) ? v : wpre[q];
+            }
           }
         }
-      }
-      if (((freeb >> lane) & 1ull) && rank < take) L.init(kp.p, kp.n_ids ? kp.ids[next + rank] : next + rank, coop ? wpre : nullptr);
-      if (((freeb >> lane) & 1ull) && rank < take) {
-        if (__builtin_expect(L.bailed, 0)) {   // (a fuzzed P above this shape's: the general kernel's)
-          const uint32_t pos = atomicAdd(kp.bail_n, 1u);
-          if (pos < kp.bail_cap) kp.bail_ids[pos] = L.gid;
-          L.mode = M_IDLE;
-          L.bailed = false;
+        if (((freeb >> lane) & 1ull) && rank < take) L.init(kp.p, kp.n_ids ? kp.ids[next + rank] : next + rank, coop ? wpre : nullptr);
+        if (((freeb >> lane) & 1ull) && rank < take) {
+          if (__builtin_expect(L.bailed, 0)) {   // (a fuzzed P above this shape's: the general kernel's)
+            const uint32_t pos = atomicAdd(kp.bail_n, 1u);
+            if (pos < kp.bail_cap) kp.bail_ids[pos] = L.gid;
+            L.mode = M_IDLE;
+            L.bailed = false;
+          }
         }
+        next += take;
+        freeb = __builtin_amdgcn_ballot_w64(L.mode == M_IDLE);
       }
-      next += take;
-      freeb = __builtin_amdgcn_ballot_w64(L.mode == M_IDLE);
+      const uint64_t idleb = __builtin_amdgcn_ballot_w64(L.mode == M_IDLE);
+      if (idleb == ~0ull) break;                   // (drained: nothing left to run)
+      nidle = (uint32_t)__popcll(idleb);
     }
-    if (__builtin_amdgcn_ballot_w64(L.mode != M_IDLE) == 0ull) break;
 
-    // ---- one iteration of every live lane ----
-    if (L.mode != M_IDLE) {
-      EvOut o;
-      const bool done = L.step(kp.p, o);
+    // ---- one iteration of every lane (idle ones inert) ----
+    EvOut o;
+    const bool done = L.step(kp.p, o, L.mode != M_IDLE);
+    if (__builtin_amdgcn_ballot_w64(done | L.bailed) != 0ull) {
       if (__builtin_expect(L.bailed, 0)) {    // beyond this kernel's capacities: re-run by the general kernel
         const uint32_t pos = atomicAdd(kp.bail_n, 1u);
         if (pos < kp.bail_cap) kp.bail_ids[pos] = L.gid;
         L.mode = M_IDLE;
         L.bailed = false;
-      } else if (__builtin_expect(done, 0)) {
+      } else if (done) {
         const uint32_t f = o.flags;
         tot.c[0] += 1u;
         tot.c[1] += (f & PXB_F_UNDECIDED) ? 1u : 0u;
@@ -266,6 +272,7 @@ __global__ __launch_bounds__(64, CMP ? 3 : SL ? 2 : 1) void paxos_ev_kernel(EvKP
           }
         }
       }
+      nidle = (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(L.mode == M_IDLE));
     }
   }
   tot.flush(trow, lane);

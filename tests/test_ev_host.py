@@ -288,3 +288,23 @@ def test_layout_words_leave_lds_to_spare(c, pm, words, blocks, monkeypatch):
     assert lib().ev_host_last_words() == words
     assert blocks * 256 * words <= 160 * 1024 - 7 * 1024
 
+
+
+# ---- the hand-derived step-schedule KATs (tests/golden/kat_step_schedule.json)
+# on the host build of the per-lane state machine: every case, whatever layout
+# its config routes to (S4/S5: faulty log mode; S6: the randomized draw) ----
+_KATS = __import__("json").load(open(os.path.join(HERE, "golden", "kat_step_schedule.json")))["cases"]
+
+
+@pytest.mark.parametrize("case", _KATS, ids=[c["name"] for c in _KATS])
+def test_step_kats_on_host(case):
+    cfg = pxb.Config(**case["config"])
+    want = case["result"]
+    res, dig, acc, cnt, bails = ev_run(cfg, case["instance"], 1)
+    assert len(bails) == 0
+    assert list(res[0]) == [want["decided_val"], want["decided_ticket"], want["rounds"],
+                            want["flags"] | (want["steps"] << 16)]
+    assert (cnt["messages"], cnt["canon_bytes"], cnt["executes"]) == \
+        (want["messages"], want["canon_bytes"], want["executes"])
+    final = [cp for cp in case["checkpoints"] if cp["step"] == want["steps"] - 1][0]
+    assert acc[0].tolist() == final["acc"]

@@ -14,6 +14,13 @@ GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 THREADS = min(16, os.cpu_count() or 1)
 
 
+def _fnv(h, v):
+    """FNV-1a-32 over the 4 little-endian bytes of v (SEMANTICS §7)."""
+    for i in range(4):
+        h = ((h ^ ((v >> (8 * i)) & 0xFF)) * 0x01000193) & 0xFFFFFFFF
+    return h
+
+
 def _cmp(cfg, first, n, want_acc=True):
     res, dig, acc, cnt = pxb.run(cfg, first, n, want_acceptors=want_acc)
     eres, edig, eacc, ecnt = oracle_c.run_cpu(cfg, first, n, threads=THREADS, want_acceptors=want_acc)
@@ -761,6 +768,15 @@ def test_step_kats_on_gpu(gpu_lib, case, production):
                             want["flags"] | (want["steps"] << 16)]
     assert (cnt["messages"], cnt["canon_bytes"], cnt["executes"]) == \
         (want["messages"], want["canon_bytes"], want["executes"])
+    final = [cp for cp in case["checkpoints"] if cp["step"] == want["steps"] - 1][0]
+    assert acc[0].tolist() == final["acc"]
+    for a, log in enumerate(want["logs"]):
+        h = 0x811C9DC5
+        for v in log:
+            h = _fnv(h, v)
+        assert int(dig[0][a]) == _fnv(h, len(log))
+    if cfg.n_ticks > 1:
+        return       # (pxb_trace_instance runs single decree only: results and records above)
     recs, tres = pxb.trace_instance(cfg, case["instance"], production=production)
     assert list(tres) == list(res[0])
     steps = [r["step"] for r in recs]
@@ -770,5 +786,3 @@ def test_step_kats_on_gpu(gpu_lib, case, production):
         assert [[int(x) for x in p[:4]] for p in r["prop"]] == cp["prop"], cp["step"]
         if "in_flight" in cp and r["in_flight"] != pxb.TRACE_IN_FLIGHT_UNKNOWN:
             assert r["in_flight"] == cp["in_flight"], cp["step"]
-    final = [cp for cp in case["checkpoints"] if cp["step"] == want["steps"] - 1][0]
-    assert acc[0].tolist() == final["acc"]

@@ -40,7 +40,7 @@ def test_draws_are_the_fixture_inputs(case):
 
 @pytest.mark.parametrize("case", KATS, ids=IDS)
 def test_python_oracle_matches_hand_derivation(case):
-    cfg = R.Config(**{**case["config"], "randomize": False})
+    cfg = R.Config(**case["config"])
     states = {}
 
     def snap(s, accs, props, in_flight):
