@@ -42,7 +42,7 @@ import           Foreign.Marshal.Utils (with)
 import           Foreign.Ptr           (Ptr, nullPtr)
 import           Foreign.Storable      (Storable (..))
 
--- | pxb_config (72 bytes, ABI 2, see include/paxos_batch.h).
+-- | pxb_config (72 bytes, ABI 3, see include/paxos_batch.h).
 data BatchConfig = BatchConfig
   { bcSeed          :: !Word64
   , bcFirst         :: !Word64   -- ^ global id of the first instance

@@ -149,10 +149,14 @@ int pxb_run(const pxb_config* cfg, pxb_result* out, uint32_t* log_digest,
  *   other fault-free (duelling proposers, log mode): the fault-free per-lane
  *     kernel for those, then the general faulty kernel over its bails;
  *   faulty single decree: the per-lane event kernel, then the general faulty
- *     kernel over its bailed instances; fuzzed three-proposer batches run the
- *     two-proposer event kernel first and the three-proposer one over the
- *     instances that drew P = 3 (chunks of 2^26; 2^25 split);
- *   faulty log mode: the general kernel (chunks up to 2^30 - 1).
+ *     kernel over its bailed instances; loss-free, skew-free batches with
+ *     delays <= 4 (BASELINE config 4) take its simple-schedule shape; fuzzed
+ *     three-proposer batches run the two-proposer event kernel first and the
+ *     three-proposer one over the instances that drew P = 3 (chunks of 2^26;
+ *     2^25 split);
+ *   faulty log mode (n_ticks > 1, delays <= 8): the per-lane event kernel's
+ *     log-mode shape, then the general log-mode kernel over its bailed
+ *     instances (chunks of 2^26; longer delays: the general log-mode kernel).
  * Each chunk
  * uses one of 64 per-device scratch slots round-robin: at most 64 chunks per
  * device may be in flight at once across streams.  A launch failure after a
@@ -176,8 +180,9 @@ int pxb_run_multi(const pxb_config* cfg, int n_devices, pxb_result* out, uint32_
  * kernels' bailed-id lists are kept per (device, stream) of pxb_run_device,
  * allocated on that stream's first faulty or per-lane launch: 16 MB each, plus
  * 64 MB for the split routing of fuzzed three-proposer batches, for at most 8
- * streams per device (a ninth stream waits for the device and takes over an
- * existing entry).  pxb_init(n) creates the launch slots of devices 0..n-1
+ * streams per device (a ninth stream takes over the oldest entry once that
+ * entry's last launches have completed: an event recorded behind them; a
+ * stream destroyed by the library hands its entry back).  pxb_init(n) creates the launch slots of devices 0..n-1
  * (n <= 0: all visible) up front; pxb_shutdown() waits for those devices, frees everything
  * and destroys the communicators; the next call starts afresh.  Both are
  * optional.  Do not call pxb_shutdown while other threads have calls in
