@@ -59,7 +59,10 @@
 namespace pxb {
 namespace ev {
 
-constexpr uint32_t PQ_CAP = 4;    // pending broadcasts per lane
+#ifndef PXB_EV_PQ_CAP
+#define PXB_EV_PQ_CAP 4
+#endif
+constexpr uint32_t PQ_CAP = PXB_EV_PQ_CAP;    // pending broadcasts per lane
 constexpr uint32_t MAX_STEP_CAP = 4095;   // 12-bit tickets (tickets <= step_cap, SEMANTICS §6)
 static_assert(MAX_STEP_CAP < PXB_TICKET_LIMIT, "EV tickets never reach the overflow limit");
 

@@ -176,14 +176,31 @@ __global__ __launch_bounds__(64, CMP ? 3 : SL ? 2 : 1) void paxos_ev_kernel(EvKP
         if (__builtin_amdgcn_ballot_w64(tot.c[0] >= EV_FLUSH) != 0ull) tot.flush(trow, lane);
         if (next >= end) {
           uint32_t c = 0;
+#ifdef PXB_EV_TAIL_GRAB
+          // Near the end of the queue a wave takes only as many instances as
+          // it has idle lanes: a 64-instance chunk taken just before the queue
+          // runs dry keeps that wave busy for about two instance lifetimes
+          // (its lanes start the chunk's instances as they free up) while the
+          // rest of the launch is already idle.  (A plain load of the queue
+          // word, in the refill path only.)
+          uint32_t grab = EV_QCHUNK;
+          {
+            const uint32_t q = (uint32_t)__builtin_amdgcn_readfirstlane(
+                (int)__atomic_load_n(kp.queue, __ATOMIC_RELAXED));
+            if (n - min(q, n) <= (uint32_t)PXB_EV_TAIL_GRAB) grab = (uint32_t)__popcll(freeb);
+          }
+          if (lane == 0) c = atomicAdd(kp.queue, grab);
+#else
+          const uint32_t grab = EV_QCHUNK;
           if (lane == 0) c = atomicAdd(kp.queue, EV_QCHUNK);
+#endif
           c = (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
           if (c >= n) {
             drained = true;
             break;
           }
           next = c;
-          end = min(c + EV_QCHUNK, n);
+          end = min(c + grab, n);
         }
         const uint32_t take = min((uint32_t)__popcll(freeb), end - next);
         const uint32_t rank = (uint32_t)__popcll(freeb & below);
@@ -235,9 +252,14 @@ __global__ __launch_bounds__(64, CMP ? 3 : SL ? 2 : 1) void paxos_ev_kernel(EvKP
       nidle = (uint32_t)__popcll(idleb);
     }
 
-    // ---- one iteration of every lane (idle ones inert) ----
+    // ---- one iteration of every live lane ----
     EvOut o;
-    const bool done = L.step(kp.p, o, L.mode != M_IDLE);
+    bool done = false;
+#ifdef PXB_EV_PRED_IDLE
+    done = L.step(kp.p, o, L.mode != M_IDLE);     // (A/B: idle lanes inert instead of masked off: -0.9 %)
+#else
+    if (L.mode != M_IDLE) done = L.step(kp.p, o);
+#endif
     if (__builtin_amdgcn_ballot_w64(done | L.bailed) != 0ull) {
       if (__builtin_expect(L.bailed, 0)) {    // beyond this kernel's capacities: re-run by the general kernel
         const uint32_t pos = atomicAdd(kp.bail_n, 1u);
