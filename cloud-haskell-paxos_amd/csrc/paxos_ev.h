@@ -471,9 +471,7 @@ struct EvLane {
   }
 
   // ---- instance start: parameters, Tick skews, isolation windows (SEMANTICS §4) ----
-  // (pre_win: the windows drawn elsewhere, by the wave's lanes together
-  // (paxos_ev_kernel.h); valid only for batches with a launch-wide crash rate)
-  __host__ __device__ __forceinline__ void init(const EvParams& kp, uint32_t g, const uint32_t* pre_win = nullptr) {
+  __host__ __device__ __forceinline__ void init(const EvParams& kp, uint32_t g) {
     gid = g;
     const uint64_t inst = kp.first_instance + g;
     lo = (uint32_t)inst;
@@ -512,8 +510,7 @@ struct EvLane {
     }
 #pragma unroll
     for (int a = 0; a < N; ++a) {
-      if (pre_win) win[a] = pre_win[a];
-      else win[a] = crashy ? window_of(kp, draw(0u, (3u << 24) | (uint32_t)a), crash_m1) : 0u;
+      win[a] = crashy ? window_of(kp, draw(0u, (3u << 24) | (uint32_t)a), crash_m1) : 0u;
       accw[a] = 0u;
       if constexpr (LG) accv[a] = 0u;
       accd[a] = 0x811C9DC5u;

@@ -163,9 +163,12 @@ __global__ __launch_bounds__(64, CMP ? 3 : SL ? 2 : 1) void paxos_ev_kernel(EvKP
   // several, and a lane ends every ~17 wave-iterations (config 4), so nearly
   // every refill started one lane; waiting for a second costs each instance
   // ~8 idle lane-iterations of its ~1090 (tools/wave_model.cpp refill_min):
-  // MI355X A/B, config 4 at 2^24: +1.3 %.  Idle lanes run the iteration with
-  // every op predicated off (step(..., act = false)), so no exec-mask branch
-  // surrounds it, and the per-iteration refill test is one scalar compare.
+  // MI355X A/B, config 4 at 2^24: +1.3 %.  The per-iteration refill test is
+  // one scalar compare.  (Measured and not kept, profiles/r04_notes: idle
+  // lanes running the iteration predicated off instead of masked, -0.9 %;
+  // the crash-window draws spread over the wave, -0.3 %; grabs of as many
+  // instances as idle lanes near the end of the queue, config 4 +-0,
+  // configs 3 and 5 -10 % (queue-word contention).)
   uint32_t nidle = 64u;
   for (;;) {
     if (nidle == 64u || (nidle >= (uint32_t)PXB_EV_REFILL_MIN && !drained)) {
@@ -176,66 +179,18 @@ __global__ __launch_bounds__(64, CMP ? 3 : SL ? 2 : 1) void paxos_ev_kernel(EvKP
         if (__builtin_amdgcn_ballot_w64(tot.c[0] >= EV_FLUSH) != 0ull) tot.flush(trow, lane);
         if (next >= end) {
           uint32_t c = 0;
-#ifdef PXB_EV_TAIL_GRAB
-          // Near the end of the queue a wave takes only as many instances as
-          // it has idle lanes: a 64-instance chunk taken just before the queue
-          // runs dry keeps that wave busy for about two instance lifetimes
-          // (its lanes start the chunk's instances as they free up) while the
-          // rest of the launch is already idle.  (A plain load of the queue
-          // word, in the refill path only.)
-          uint32_t grab = EV_QCHUNK;
-          {
-            const uint32_t q = (uint32_t)__builtin_amdgcn_readfirstlane(
-                (int)__atomic_load_n(kp.queue, __ATOMIC_RELAXED));
-            if (n - min(q, n) <= (uint32_t)PXB_EV_TAIL_GRAB) grab = (uint32_t)__popcll(freeb);
-          }
-          if (lane == 0) c = atomicAdd(kp.queue, grab);
-#else
-          const uint32_t grab = EV_QCHUNK;
           if (lane == 0) c = atomicAdd(kp.queue, EV_QCHUNK);
-#endif
           c = (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
           if (c >= n) {
             drained = true;
             break;
           }
           next = c;
-          end = min(c + grab, n);
+          end = min(c + EV_QCHUNK, n);
         }
         const uint32_t take = min((uint32_t)__popcll(freeb), end - next);
         const uint32_t rank = (uint32_t)__popcll(freeb & below);
-        // Isolation windows of a launch-wide crash rate: the N draws of each
-        // instance taken are spread over the wave's lanes (one draw per lane for
-        // up to 64 / N instances) instead of N serial draws in the lanes that
-        // start one: a refill serves ~1 lane (a lane ends every ~17 wave-
-        // iterations), so the wave ran all N draws for it (config 4: ~300 of the
-        // ~600 instructions of a refill; tools/wave_model.cpp, tools/isa_budget.py)
-        uint32_t wpre[N] = {};
-  #ifdef PXB_EV_COOP_WIN
-        const bool coop = (kp.p.cfg & (EV_CFG_CRASHY | EV_CFG_RANDOMIZE)) == EV_CFG_CRASHY;
-  #else
-        const bool coop = false;            // (MI355X A/B, config 4: -0.3 %: not used)
-  #endif
-        if (coop) {
-          const uint32_t nd = take * (uint32_t)N;
-          for (uint32_t base = 0; base < nd; base += 64u) {          // (wave-uniform)
-            const uint32_t d = base + lane;
-            const uint32_t r = d / (uint32_t)N, a = d - r * (uint32_t)N;
-            uint32_t wv = 0u;
-            if (d < nd) {
-              const uint64_t inst = kp.p.first_instance + (kp.n_ids ? kp.ids[next + r] : next + r);
-              const uint4 w = philox_rk((uint32_t)inst, (uint32_t)(inst >> 32), 0u, (3u << 24) | a, L.rk);
-              wv = decltype(L)::window_of(kp.p, w, kp.p.crash_m1);
-            }
-  #pragma unroll
-            for (int q = 0; q < N; ++q) {
-              const uint32_t src = rank * (uint32_t)N + (uint32_t)q - base;   // (wraps below base)
-              const uint32_t v = (uint32_t)__shfl((int)wv, (int)(src & 63u), 64);
-              wpre[q] = (src < 64u) ? v : wpre[q];
-            }
-          }
-        }
-        if (((freeb >> lane) & 1ull) && rank < take) L.init(kp.p, kp.n_ids ? kp.ids[next + rank] : next + rank, coop ? wpre : nullptr);
+        if (((freeb >> lane) & 1ull) && rank < take) L.init(kp.p, kp.n_ids ? kp.ids[next + rank] : next + rank);
         if (((freeb >> lane) & 1ull) && rank < take) {
           if (__builtin_expect(L.bailed, 0)) {   // (a fuzzed P above this shape's: the general kernel's)
             const uint32_t pos = atomicAdd(kp.bail_n, 1u);
@@ -255,11 +210,7 @@ __global__ __launch_bounds__(64, CMP ? 3 : SL ? 2 : 1) void paxos_ev_kernel(EvKP
     // ---- one iteration of every live lane ----
     EvOut o;
     bool done = false;
-#ifdef PXB_EV_PRED_IDLE
-    done = L.step(kp.p, o, L.mode != M_IDLE);     // (A/B: idle lanes inert instead of masked off: -0.9 %)
-#else
     if (L.mode != M_IDLE) done = L.step(kp.p, o);
-#endif
     if (__builtin_amdgcn_ballot_w64(done | L.bailed) != 0ull) {
       if (__builtin_expect(L.bailed, 0)) {    // beyond this kernel's capacities: re-run by the general kernel
         const uint32_t pos = atomicAdd(kp.bail_n, 1u);
