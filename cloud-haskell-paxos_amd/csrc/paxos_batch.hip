@@ -768,6 +768,11 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
       }
       const uint64_t eres = (uint64_t)eocc * (uint64_t)cus;
       const unsigned egrid = (unsigned)std::min<uint64_t>((nc + 63) / 64, eres);
+#ifdef PXB_WAVE_TIMES
+      if (!g_wt) HIPCHK(hipMalloc(&g_wt, 6ull * 65536 * sizeof(unsigned long long)));
+      ek.dbg = g_wt;
+      g_wt_waves = egrid;
+#endif
       hipLaunchKernelGGL(efn, dim3(egrid), dim3(64), 0, st, ek);
       if (hipError_t e = hipGetLastError()) return fail(e);
       kp.ids = bail;

@@ -59,6 +59,9 @@ struct EvKParams {
   const uint32_t* ids;
   const uint32_t* n_ids;
   uint32_t ids_cap;
+#ifdef PXB_WAVE_TIMES
+  unsigned long long* dbg;                    // diagnostic: per-wave (start, end, last grab, instances, HW_ID, XCC_ID)
+#endif
 };
 
 // response-pool words per lane of a shape (the compact layout is picked for
@@ -152,6 +155,11 @@ __global__ __launch_bounds__(64, CMP ? 3 : SL ? 2 : 1) void paxos_ev_kernel(EvKP
   const uint64_t below = (1ull << lane) - 1ull;
   uint32_t next = 0, end = 0;
   bool drained = false;
+#ifdef PXB_WAVE_TIMES   // diagnostic: wave start / end / last chunk grab (100 MHz constant clock), instances taken
+  const uint64_t wt0 = __builtin_amdgcn_s_memrealtime();
+  uint64_t wgrab = wt0;
+  uint32_t wtaken = 0;
+#endif
 
 #ifndef PXB_EV_REFILL_MIN
 #define PXB_EV_REFILL_MIN 2
@@ -187,6 +195,10 @@ __global__ __launch_bounds__(64, CMP ? 3 : SL ? 2 : 1) void paxos_ev_kernel(EvKP
           }
           next = c;
           end = min(c + EV_QCHUNK, n);
+#ifdef PXB_WAVE_TIMES
+          wgrab = __builtin_amdgcn_s_memrealtime();
+          wtaken += EV_QCHUNK;
+#endif
         }
         const uint32_t take = min((uint32_t)__popcll(freeb), end - next);
         const uint32_t rank = (uint32_t)__popcll(freeb & below);
@@ -248,6 +260,16 @@ __global__ __launch_bounds__(64, CMP ? 3 : SL ? 2 : 1) void paxos_ev_kernel(EvKP
       nidle = (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(L.mode == M_IDLE));
     }
   }
+#ifdef PXB_WAVE_TIMES
+  if (kp.dbg && blockIdx.x < 65536u) {
+    const uint64_t wt1 = __builtin_amdgcn_s_memrealtime();
+    const uint64_t hw = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);
+    const uint64_t xcc = (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 20);
+    if (lane < 6)
+      kp.dbg[6ull * blockIdx.x + lane] = lane == 0 ? wt0 : lane == 1 ? wt1 : lane == 2 ? wgrab : lane == 3 ? wtaken
+                                        : lane == 4 ? hw : xcc;
+  }
+#endif
   tot.flush(trow, lane);
 }
 

@@ -1068,7 +1068,9 @@ __global__ __launch_bounds__((Shape<PM, N, LOGM, FF>::block), (Occ<PM, FF>::wave
     // HW_ID (SIMD, CU, SE fields) and XCC_ID hardware registers
     const uint64_t hw = (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);
     const uint64_t xcc = (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 20);
-    if (lane < 6)
+    // (only launches given a buffer: the general kernel behind the per-lane
+    // kernels runs with kp.dbg null -- an unguarded store here faulted)
+    if (kp.dbg && lane < 6 && wave < 65536u)
       kp.dbg[6 * wave + lane] = lane == 0 ? wt0 : lane == 1 ? wt1 : lane == 2 ? hw : lane == 3 ? xcc : lane == 4 ? wm0 : wm1;
   }
 #endif
