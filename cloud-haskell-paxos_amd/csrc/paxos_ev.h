@@ -1038,7 +1038,17 @@ struct EvLane {
 
   // final per-acceptor outputs (digest, record) of an ended instance
   __host__ __device__ uint32_t log_len_of(int a) const { return (LG ? accv[LG ? a : 0] : accw[a]) >> A_LEN; }
-  __host__ __device__ uint32_t digest_of(int a) const { return fnv_u32(accd[a], log_len_of(a)); }
+  // (single decree: log lengths < 32 fit the first byte, so FNV-1a over the
+  // bytes (len, 0, 0, 0) is (h ^ len) * prime^4)
+  __host__ __device__ uint32_t digest_of(int a) const {
+    if constexpr (LG) {
+      return fnv_u32(accd[a], log_len_of(a));
+    } else {
+      constexpr uint32_t P = 0x01000193u, P2 = P * P, P4 = P2 * P2;
+      static_assert(A_LEN_MAX < 256, "one-byte log length");
+      return (accd[a] ^ log_len_of(a)) * P4;
+    }
+  }
   __host__ __device__ void record_of(int a, uint32_t r[4]) const {
     const uint32_t A = accw[a];
     const uint32_t val = LG ? accv[LG ? a : 0] & 0x3FFFu : (A >> 24) & 3u;
