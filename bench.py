@@ -96,32 +96,51 @@ def scaling_of(c: int) -> str:
 
 class GpuLeg:
     """The measured work of one rank: pxb_run_device over fresh instance ids,
-    asynchronous on one HIP stream, timed with an event pair on that stream."""
+    asynchronous, timed with an event pair.  Consecutive steps alternate
+    between two HIP streams with their own output buffers (double buffering):
+    the per-lane kernel is persistent (its grid is the resident capacity), so
+    step k + 1's waves are dispatched onto the CUs that step k's last waves free
+    up -- its tail (the slowest instances of the last waves, then the general
+    kernel over its bailed ones: 2.5 % + 1 % of a 2^23-instance step,
+    tools/ev_wave_times.py) overlaps the next step's work instead of idling
+    the GPU.  All K steps still complete inside the timed region."""
 
     def __init__(self, cfg, n, rank, world, stream, dev, outputs=True):
         import torch
         import pxb
         self.torch, self.pxb = torch, pxb
         self.cfg, self.n, self.rank, self.world, self.stream, self.dev = cfg, n, rank, world, stream, dev
+        self.streams = [stream, torch.cuda.Stream(dev)]
         # (outputs=False: run totals only, no per-instance records)
-        self.out = torch.empty((n, 4), dtype=torch.int32, device=dev) if outputs else None
-        self.dig = torch.empty((n, cfg.n_acceptors), dtype=torch.int32, device=dev) if outputs else None
+        self.out = [torch.empty((n, 4), dtype=torch.int32, device=dev) if outputs else None for _ in range(2)]
+        self.dig = [torch.empty((n, cfg.n_acceptors), dtype=torch.int32, device=dev) if outputs else None
+                    for _ in range(2)]
         self.tot = torch.zeros(16, dtype=torch.int64, device=dev)
         self.e0 = torch.cuda.Event(enable_timing=True)
         self.e1 = torch.cuda.Event(enable_timing=True)
 
     def launch(self, step, count):
         first = (step * self.world + self.rank) * self.n      # fresh global instance ids per step/rank
-        with self.torch.cuda.stream(self.stream):
-            self.pxb.run_device(self.cfg, first, count, d_results=self.out, d_digests=self.dig, d_totals=self.tot,
-                                stream=self.stream.cuda_stream)
+        k = step & 1
+        st = self.streams[k]
+        with self.torch.cuda.stream(st):
+            self.pxb.run_device(self.cfg, first, count, d_results=self.out[k], d_digests=self.dig[k],
+                                d_totals=self.tot, stream=st.cuda_stream)
 
     def sync(self):
         self.torch.cuda.synchronize()
 
     def mark(self, which):
-        # (e1 - e0) / K is the mean step time on the launch stream, gaps between kernels included
-        (self.e0 if which == 0 else self.e1).record(self.stream)
+        # (e1 - e0) / K is the mean step time over both streams, gaps between kernels included
+        a, b = self.streams
+        if which == 0:
+            self.e0.record(a)
+            b.wait_event(self.e0)
+        else:
+            done_b = self.torch.cuda.Event()
+            done_b.record(b)
+            a.wait_event(done_b)
+            self.e1.record(a)
 
     def event_ms(self):
         return self.e0.elapsed_time(self.e1)
