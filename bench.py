@@ -44,6 +44,7 @@ VALU_PEAK_G = CUS * 2 * 2.4  # G wave64 VALU instructions / s (1228.8)
 PROFILES = os.path.join(ROOT, "profiles")
 PROFILE_ROUNDS = ("r04", "r03", "r02")   # the newest committed profile set of a workload wins
 BATCHES_PER_STEP = 256       # config-2 batches of 2^20 per timed step (>= 100 ms over 20 steps)
+ONE_STREAM = False           # --one-stream (A/B)
 DRY_NORTH_STAR = 1 << 12     # --dry-run stand-in for the headline's 2^26 instances per step
 
 
@@ -61,6 +62,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true")
     ap.add_argument("--dry-run", action="store_true", help="CPU ranks (gloo), synthetic work: launcher test only")
+    ap.add_argument("--one-stream", action="store_true",
+                    help="all steps on one stream (A/B of the two-stream step pipeline)")
     return ap.parse_args()
 
 
@@ -110,7 +113,7 @@ class GpuLeg:
         import pxb
         self.torch, self.pxb = torch, pxb
         self.cfg, self.n, self.rank, self.world, self.stream, self.dev = cfg, n, rank, world, stream, dev
-        self.streams = [stream, torch.cuda.Stream(dev)]
+        self.streams = [stream, stream if ONE_STREAM else torch.cuda.Stream(dev)]
         # (outputs=False: run totals only, no per-instance records)
         self.out = [torch.empty((n, 4), dtype=torch.int32, device=dev) if outputs else None for _ in range(2)]
         self.dig = [torch.empty((n, cfg.n_acceptors), dtype=torch.int32, device=dev) if outputs else None
@@ -446,6 +449,8 @@ def main():
     import torch.distributed as dist
     if args.dry_run:
         return dry_main(args, rank, world)
+    global ONE_STREAM
+    ONE_STREAM = args.one_stream
     import pxb
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))

@@ -47,6 +47,20 @@ def main():
     print("the last 10 %% of waves to end: last grab at %.3f ms (median), end %.3f ms (median)" % (
         np.median(grab[late]), np.median(end[late])))
     print("totals", pxb.counters_dict(tot.cpu().tolist())["instances"])
+    # placement: HW_ID = wave [3:0] simd [5:4] cu [11:8] sh [12] se [15:13]; XCC_ID [3:0]
+    hw = buf[:nw, 4].astype(np.int64)
+    xcc = buf[:nw, 5].astype(np.int64) & 15
+    simd = (hw >> 4) & 3
+    cu = (xcc << 8) | (((hw >> 13) & 7) << 5) | (((hw >> 12) & 1) << 4) | ((hw >> 8) & 15)
+    key = cu * 4 + simd
+    _, inv, cnt = np.unique(key, return_inverse=True, return_counts=True)
+    per_simd = cnt[inv]                     # waves sharing this wave's SIMD
+    ncu = len(np.unique(cu))
+    print("CUs used %d, SIMDs used %d; waves per CU: %s" % (ncu, len(cnt), np.bincount(np.unique(cu, return_counts=True)[1])))
+    for k in sorted(set(per_simd.tolist())):
+        m = per_simd == k
+        print("waves on SIMDs shared by %d: %4d waves, instances per wave mean %.0f (min %d max %d), "
+              "per-SIMD rate %.0f" % (k, m.sum(), taken[m].mean(), taken[m].min(), taken[m].max(), k * taken[m].mean()))
 
 
 if __name__ == "__main__":
