@@ -267,7 +267,13 @@ struct EvLane {
   uint32_t tper;                      // LG: steps between Ticks
   uint32_t nsent[PM];                 // broadcasts of p whose copies have started (request-link seq)
   uint32_t bnext[PM];                 // next broadcast-ring slot
-  uint32_t refc[PM];                  // ring-slot reference counts (4-bit nibbles)
+  // ring-slot reference counts, 4-bit nibbles: one 32- or 64-bit word for
+  // every proposer when they fit (nibble p * BR + slot: an add, no one-hot
+  // select), else a word each
+  static constexpr bool RPK = PM * S::BR * 4 <= 64;
+  using ref_t = typename std::conditional<(PM * S::BR * 4 > 32), unsigned long long, uint32_t>::type;
+  ref_t refp;
+  uint32_t refc[RPK ? 1 : PM];
   // acceptor states (Server.hs:24-31), isolation windows, log digests
   uint32_t accw[N], win[N], accd[N];
   uint32_t accv[LG ? N : 1];          // LG: the stored command and log length of each acceptor
@@ -357,6 +363,16 @@ struct EvLane {
   template <int K>
   __host__ __device__ static __forceinline__ void put(uint32_t (&v)[K], uint32_t q, uint32_t x) {
     set_from<K>(v, 1u << q, x);
+  }
+
+  // the reference-count nibble of q's ring slot k, and adding d to it
+  __host__ __device__ __forceinline__ uint32_t ref_nib(uint32_t q, uint32_t k) const {
+    return RPK ? (uint32_t)(refp >> (4u * (q * (uint32_t)S::BR + k))) & 15u : (get(refc, q) >> (4u * k)) & 15u;
+  }
+  // (d: 1, 0 or ~0u = -1)
+  __host__ __device__ __forceinline__ void ref_add(uint32_t q, uint32_t k, uint32_t d) {
+    if constexpr (RPK) refp += (ref_t)(typename std::make_signed<ref_t>::type)(int32_t)d << (4u * (q * (uint32_t)S::BR + k));
+    else put(refc, q, get(refc, q) + (d << (4u * k)));
   }
 
   // a value as the reference's command code (id << 24) | t (SEMANTICS §2)
@@ -506,7 +522,9 @@ struct EvLane {
       const int32_t lt = (int32_t)(((uint32_t)p < P) ? tk_end[p] : 0u);
       last_tick = (lt > last_tick) ? lt : last_tick;
       pw0[p] = pw1[p] = pw2[p] = 0u;               // ticket 0, Idle, no command (Client.hs:90-95)
-      nsent[p] = bnext[p] = refc[p] = 0u;
+      nsent[p] = bnext[p] = 0u;
+      refc[RPK ? 0 : p] = 0u;
+      refp = 0u;
     }
 #pragma unroll
     for (int a = 0; a < N; ++a) {
@@ -567,11 +585,10 @@ struct EvLane {
     dval = first ? val : dval;
     dtick = first ? x0 : dtick;
     const uint32_t slot0 = get(bnext, q), slot1 = (slot0 + 1u) & (S::BR - 1u);
-    const uint32_t rc = get(refc, q);
     // a ring slot still referenced by a queued copy
     // (non-short-circuit: || here became two exec-mask branches)
-    bailed = bailed | (p0 & (((rc >> (4u * slot0)) & 15u) != 0u)) | (p1 & (((rc >> (4u * slot1)) & 15u) != 0u));
-    PXB_EV_PROBE(EVB_RING, (p0 & (((rc >> (4u * slot0)) & 15u) != 0u)) | (p1 & (((rc >> (4u * slot1)) & 15u) != 0u)));
+    bailed = bailed | (p0 & (ref_nib(q, slot0) != 0u)) | (p1 & (ref_nib(q, slot1) != 0u));
+    PXB_EV_PROBE(EVB_RING, (p0 & (ref_nib(q, slot0) != 0u)) | (p1 & (ref_nib(q, slot1) != 0u)));
     PXB_EV_PROBE(EVP_BCAST, p0);
     if (p0) {                                        // (p1 only with p0)
       if constexpr (LG) {
@@ -671,7 +688,7 @@ struct EvLane {
                                : ((wv + (1u << S::RL) + (ent << (S::IB * len))) & ~(15u << RD)) | (due4 << RD);
     const uint32_t nQ = wv + (1u << S::QL) + ((cslot | ((due4 & DM) << S::SB)) << ((uint32_t)S::EB * len));
     m.st(lw, go ? (isR ? nR : nQ) : wv);
-    put(refc, cp, get(refc, cp) + ((go & !isR) ? 1u << (4u * cslot) : 0u));
+    ref_add(cp, cslot, (go & !isR) ? 1u : 0u);
     // a carried copy due now joins this step's due links, the rest the wheel
     const bool now = EARLY & !isR & (base + due_rel == (uint32_t)s);
     const uint32_t slot = (base + due_rel) & WM;
@@ -720,7 +737,7 @@ struct EvLane {
     // (inactive lanes store their word back unchanged)
     // (entries above the length are 0: a pop shifts zeros in; a full FIFO bails)
     m.st(S::REQ + Lq, go ? wq + (1u << S::QL) + (ent << ((uint32_t)S::EB * qlen)) : wq);
-    put(refc, cp, get(refc, cp) + (go ? 1u << (4u * cslot) : 0u));
+    ref_add(cp, cslot, go ? 1u : 0u);
     // due at s (a carried-over copy with the shortest delay): straight into
     // this step's due links, else into the wheel
     const bool now = EARLY & (sb + due_rel == (uint32_t)s);
@@ -794,7 +811,7 @@ struct EvLane {
       const uint32_t w16 = m.ld16h(S::BRING + bring_word(p, bslot), bring_half(p, bslot));
       kind = w16 >> 14, x = w16 & 0xFFFu, z = (w16 >> 12) & 3u;
     }
-    put(refc, p, get(refc, p) - (acc ? 1u << (4u * bslot) : 0u));
+    ref_add(p, bslot, acc ? ~0u : 0u);
     const uint32_t A = get(accw, a);
     const bool dead = ((A >> A_DEAD) & 1u) != 0u;
     const uint32_t wa = get(win, a);                 // isolated at s: c0 <= s < c1 (SEMANTICS §4)

@@ -94,6 +94,8 @@ def main() -> None:
             continue
         cur[2].append(t.split()[0])
     nasm = sum(len(b[2]) for b in blocks)
+    res = [l.strip("; \n") for l in open(asm) if re.match(r"^\s*; (NumVgprs|NumAgprs|TotalNumVgprs|NumSgprs|ScratchSize|Occupancy):", l)]
+    print("resources: " + ", ".join(res[:6]))
 
     # ---- instruction addresses from the object ----
     dis = subprocess.run([os.path.join(LLVM, "llvm-objdump"), "-d", "--no-show-raw-insn", elf],
