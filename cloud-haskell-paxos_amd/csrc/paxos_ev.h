@@ -255,7 +255,11 @@ struct EvLane {
   int32_t s, last_tick;
   uint32_t acc_mask;                  // this step's request links with due messages left
   uint32_t in_mask;                   // this step's proposer inputs left (Tick / response links)
-  uint32_t occ;                       // wheel slots holding due bits
+  // wheel slots holding due bits, twice (bits k and W + k): the slots from
+  // any step on are one bit-field extract
+  uint32_t occ;
+  static constexpr uint32_t OCC1 = 1u | (1u << W);
+  static_assert(2 * W <= 32, "doubled wheel occupancy");
   // proposer states (ClientState, Client.hs:58-67), packed (tickets < 2^12,
   // commands = clientId, acks <= N/2 + 1):
   //   pw0 = ticket [11:0] | mr_t [23:12] | acks [27:24] | state [29:28] | pending [30]
@@ -429,7 +433,7 @@ struct EvLane {
       m.st(S::WHEEL + 2u * slot + 1u, 0u);
     }
     m.st(S::WHEEL + S::WW * slot, 0u);
-    occ &= ~(1u << slot);
+    occ &= ~(OCC1 << slot);
     acc_mask = wq;
     // Ticks only up to the last skew
     uint32_t tk = 0u;
@@ -693,7 +697,7 @@ struct EvLane {
     const bool now = EARLY & !isR & (base + due_rel == (uint32_t)s);
     const uint32_t slot = (base + due_rel) & WM;
     m.orw(S::WHEEL + slot * S::WW + ((S::WW == 2 && isR) ? 1u : 0u), (go & !now) ? 1u << (isR ? rp.bit : Lq) : 0u);
-    occ |= (go & !now) ? (1u << slot) : 0u;
+    occ |= (go & !now) ? (OCC1 << slot) : 0u;
     acc_mask |= (go & now) ? (1u << Lq) : 0u;
   }
 
@@ -743,7 +747,7 @@ struct EvLane {
     const bool now = EARLY & (sb + due_rel == (uint32_t)s);
     const uint32_t slot = (sb + due_rel) & WM;
     m.orw(S::WHEEL + slot * S::WW, (go & !now) ? 1u << Lq : 0u);
-    occ |= (go & !now) ? (1u << slot) : 0u;
+    occ |= (go & !now) ? (OCC1 << slot) : 0u;
     acc_mask |= (go & now) ? (1u << Lq) : 0u;
   }
 
@@ -1005,7 +1009,7 @@ struct EvLane {
       const bool back = EARLY & !SP & (canon == canon0);
       // the next step with a due message or a Tick (skews of absent proposers are 0)
       const uint32_t s1 = (uint32_t)s + 1u;
-      const uint32_t rot = ((occ >> (s1 & WM)) | (occ << ((W - (s1 & WM)) & WM))) & ((1u << W) - 1u);
+      const uint32_t rot = (occ >> (s1 & WM)) & ((1u << W) - 1u);   // (occupied slots from s1 on)
       uint32_t nx = ((occ != 0u) & (pq_len == 0u)) ? s1 + ctz32(rot) : (pq_len ? s1 : 0xFFFFu);
       PXB_EV_PROBE(EVP_TICK_END, s < last_tick);
       if (!SP && any_lane(s < last_tick)) {           // (a later Tick: first steps only)
