@@ -130,6 +130,16 @@ class GpuLeg:
             self.pxb.run_device(self.cfg, first, count, d_results=self.out[k], d_digests=self.dig[k],
                                 d_totals=self.tot, stream=st.cuda_stream)
 
+    def prime(self):
+        # one small launch on each stream before the warmup steps: the library's
+        # per-stream state (bail and split lists) is allocated on a stream's
+        # first launch, which must not fall inside the timed region when the
+        # warmup steps (W = 1) touch only the first stream
+        for k, st in enumerate(self.streams):
+            with self.torch.cuda.stream(st):
+                self.pxb.run_device(self.cfg, 1 << 48, min(self.n, 1 << 12), d_results=self.out[k],
+                                    d_digests=self.dig[k], d_totals=self.tot, stream=st.cuda_stream)
+
     def sync(self):
         self.torch.cuda.synchronize()
 
@@ -182,6 +192,8 @@ def run_workload(leg, n, steps, warmup, world, warm_n=None):
     from the leg's events; run totals summed over ranks)."""
     import torch
     import torch.distributed as dist
+    if hasattr(leg, "prime"):
+        leg.prime()
     for w in range(warmup):
         leg.launch(w, warm_n or n)
     leg.sync()
