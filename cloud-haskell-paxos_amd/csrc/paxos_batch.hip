@@ -392,7 +392,8 @@ static int list_used(EvLists* e, hipStream_t st) {
 // A stream that is about to be destroyed gives up its lists (paxos_multi.cpp
 // creates a stream per device and call): the entry is freed for the next stream
 // (which waits for the event first), so lists never outlive their stream's use.
-extern "C" void pxb_stream_release(int dev, hipStream_t st) {
+extern "C" void pxb_stream_release(int dev, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
   if (dev < 0 || dev >= 64 || !st) return;
   std::lock_guard<std::mutex> lk(g_mu);
   for (int k = 0; k < g_nlists[dev]; ++k)

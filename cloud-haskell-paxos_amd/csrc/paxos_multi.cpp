@@ -79,7 +79,6 @@ bool injected(const char* phase, int g) {
   return p && d && strcmp(p, phase) == 0 && atoi(d) == g;
 }
 
-extern "C" void pxb_stream_release(int dev, hipStream_t st);   // paxos_batch.hip
 
 struct HipShards {
   const pxb_config* cfg;

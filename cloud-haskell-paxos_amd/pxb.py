@@ -207,6 +207,8 @@ def load(path: str = LIB_PATH):
                        ("pxb_trace_instance", [vp, C.c_uint64, vp, C.c_uint32, vp, vp])):
         getattr(lib, name).argtypes = args
         getattr(lib, name).restype = C.c_int
+    lib.pxb_stream_release.argtypes = [C.c_int, vp]
+    lib.pxb_stream_release.restype = None
     _lib = lib
     return lib
 
@@ -405,6 +407,12 @@ def trace_instance(cfg: Config, instance: int, max_records: int = 8192, producti
 def init(n_devices: int = 0):
     """pxb_init: allocate the per-device scratch of devices 0..n-1 up front."""
     check(load().pxb_init(n_devices))
+
+
+def stream_release(dev: int, stream: int):
+    """pxb_stream_release: a stream used with run_device is about to be
+    destroyed; its bailed-id lists go back to the library."""
+    load().pxb_stream_release(dev, C.c_void_p(stream))
 
 
 def shutdown():

@@ -192,6 +192,15 @@ int pxb_run_multi(const pxb_config* cfg, int n_devices, pxb_result* out, uint32_
 int pxb_init(int n_devices);
 int pxb_shutdown(void);
 
+/* pxb_stream_release: `stream` (a hipStream_t used with pxb_run_device on device
+ * `dev`) is about to be destroyed: its bailed-id lists go back to the library
+ * for the next stream, which first waits for the event behind their last
+ * launches.  Optional (without it a ninth stream takes the oldest entry over);
+ * pxb_run_multi calls it for the streams it creates.  Unknown streams are
+ * ignored.  First use of a stream allocates its lists: a timed loop should
+ * make one small untimed launch on every stream it will use (bench.py does).  */
+void pxb_stream_release(int dev, void* stream);
+
 /* ---- per-instance trace (the build counterpart of the reference's `say`
  * state dumps, Server.hs:85 and Client.hs:108) ---------------------------------
  * Runs ONE instance of a single-decree batch on the current device through the

@@ -109,6 +109,8 @@ def test_init_and_shutdown_without_gpu():
     assert lib.pxb_init(0) == pxb.PXB_E_NODEV
     assert lib.pxb_shutdown() == pxb.PXB_OK
     assert lib.pxb_shutdown() == pxb.PXB_OK
+    pxb.stream_release(0, 0x1234)              # (a stream the library never saw: ignored)
+    pxb.stream_release(-1, 0)
 
 
 def test_multi_without_gpu_fails_loudly():

@@ -530,6 +530,30 @@ def test_run_multi_repeated_calls_release_stream_lists(gpu_lib):
         assert np.array_equal(res, want[0]) and np.array_equal(dig, want[1]) and cnt == want[3]
 
 
+def test_stream_release_with_caller_streams(gpu_lib):
+    """pxb_stream_release through the public ABI: 12 caller-created streams in
+    turn (more than a device's 8 list entries), each released before the next
+    is made, on config 5's split routing (both list kinds) and config 4; every
+    batch matches the one made on the default stream."""
+    import torch
+    for c in (5, 4):
+        cfg = pxb.CONFIGS[c]
+        want = pxb.run(cfg, 77, 6000)
+        for _ in range(12):
+            st = torch.cuda.Stream()
+            out = torch.empty((6000, 4), dtype=torch.int32, device="cuda")
+            dig = torch.empty((6000, cfg.n_acceptors), dtype=torch.int32, device="cuda")
+            tot = torch.zeros(16, dtype=torch.int64, device="cuda")
+            pxb.run_device(cfg, 77, 6000, d_results=out, d_digests=dig, d_totals=tot, stream=st.cuda_stream)
+            st.synchronize()
+            pxb.stream_release(torch.cuda.current_device(), st.cuda_stream)
+            assert np.array_equal(out.cpu().numpy().view(np.uint32), want[0])
+            assert np.array_equal(dig.cpu().numpy().view(np.uint32), want[1])
+            assert pxb.counters_dict(tot.cpu().tolist()) == want[3]
+            del st
+        pxb.stream_release(0, 0)                  # (unknown / null streams are ignored)
+
+
 def test_config5_full_sweep_totals(gpu_lib):
     """BASELINE config 5 at its stated size: all 2^28 randomized schedules on
     one GPU in one call (run totals only, no per-instance outputs).  The
