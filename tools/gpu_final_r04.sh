@@ -19,7 +19,9 @@ prof() {   # <config> <instances per step> <steps> <warmup>
   cp $(find gpurun_out/fin4/config$1/write -name '*counter_collection.csv' | head -1) $D/pmc_write.csv
   mkdir -p profiles && rm -rf profiles/r04_config$1 && cp -r $D profiles/   # (the bench below reads them)
 }
-prof 4 67108864 1 1 && prof 2 268435456 2 1 && prof 3 16777216 1 1 && prof 5 33554432 1 1 && prof 7 4194304 2 1 || exit 1
+# (two warmup steps and one stream, tools/profile_set.sh: every dispatch of a kernel is the same
+# size and runs alone, so rocprof's average duration is the per-launch kernel time)
+prof 4 67108864 1 2 && prof 2 268435456 2 2 && prof 3 16777216 1 2 && prof 5 33554432 1 2 && prof 7 4194304 2 2 || exit 1
 timeout -k 10 600 python3 -u bench.py > gpurun_out/fin4/bench.json 2> gpurun_out/fin4/bench.err || { tail -20 gpurun_out/fin4/bench.err; exit 1; }
 cp gpurun_out/fin4/bench.json gpurun_out/fin4/prof/r04_bench.json
 python3 -c "

@@ -9,7 +9,9 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/$1; C=$2; NI=$3; S=$4; W=$5
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-ARGS="--no-cpu --no-extra --config $C --instances $NI --steps $S --warmup $W"
+# (--one-stream: with bench.py's two step streams a launch queued behind another is
+# dispatched early and rocprof's duration for it includes the wait for CUs)
+ARGS="--no-cpu --no-extra --one-stream --config $C --instances $NI --steps $S --warmup $W"
 timeout -s KILL 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python3 $R/bench.py $ARGS > $OUT/bench.json 2> $OUT/trace.log || { tail -5 $OUT/trace.log; exit 1; }
 echo "trace done"
 timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE -d $OUT/valu -o pmc --output-format csv -- python3 $R/bench.py $ARGS > $OUT/valu.log 2>&1 || { tail -5 $OUT/valu.log; exit 1; }
