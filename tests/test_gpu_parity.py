@@ -497,9 +497,10 @@ def test_many_streams_concurrent(gpu_lib):
             out = torch.zeros((n, 4), dtype=torch.int32, device="cuda")
             dig = torch.zeros((n, cfg.n_acceptors), dtype=torch.int32, device="cuda")
             tot = torch.zeros(16, dtype=torch.int64, device="cuda")
+            torch.cuda.current_stream().synchronize()     # (the zeros above are on this thread's stream)
             for _ in range(2):
-                tot.zero_()
                 with torch.cuda.stream(st):
+                    tot.zero_()                           # (on st: ordered before the launch)
                     pxb.run_device(cfg, 100000 * t, n, d_results=out, d_digests=dig, d_totals=tot,
                                    stream=st.cuda_stream)
                 st.synchronize()
@@ -544,6 +545,7 @@ def test_stream_release_with_caller_streams(gpu_lib):
             out = torch.empty((6000, 4), dtype=torch.int32, device="cuda")
             dig = torch.empty((6000, cfg.n_acceptors), dtype=torch.int32, device="cuda")
             tot = torch.zeros(16, dtype=torch.int64, device="cuda")
+            torch.cuda.current_stream().synchronize()     # (zeros before the launch on st)
             pxb.run_device(cfg, 77, 6000, d_results=out, d_digests=dig, d_totals=tot, stream=st.cuda_stream)
             st.synchronize()
             pxb.stream_release(torch.cuda.current_device(), st.cuda_stream)
