@@ -44,7 +44,7 @@ VALU_PEAK_G = CUS * 2 * 2.4  # G wave64 VALU instructions / s (1228.8)
 PROFILES = os.path.join(ROOT, "profiles")
 PROFILE_ROUNDS = ("r04", "r03", "r02")   # the newest committed profile set of a workload wins
 BATCHES_PER_STEP = 256       # config-2 batches of 2^20 per timed step (>= 100 ms over 20 steps)
-ONE_STREAM = False           # --one-stream (A/B)
+STEP_STREAMS = 0             # --streams (A/B; --one-stream = 1; 0: by step size, GpuLeg)
 DRY_NORTH_STAR = 1 << 12     # --dry-run stand-in for the headline's 2^26 instances per step
 
 
@@ -62,6 +62,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true")
     ap.add_argument("--dry-run", action="store_true", help="CPU ranks (gloo), synthetic work: launcher test only")
+    ap.add_argument("--streams", type=int, default=0, help="step streams (default: 2 up to 2^24 instances per step, else 1)")
     ap.add_argument("--one-stream", action="store_true",
                     help="all steps on one stream (A/B of the two-stream step pipeline)")
     return ap.parse_args()
@@ -99,32 +100,39 @@ def scaling_of(c: int) -> str:
 
 class GpuLeg:
     """The measured work of one rank: pxb_run_device over fresh instance ids,
-    asynchronous, timed with an event pair.  Consecutive steps alternate
-    between two HIP streams with their own output buffers (double buffering):
-    the per-lane kernel is persistent (its grid is the resident capacity), so
-    step k + 1's waves are dispatched onto the CUs that step k's last waves free
-    up -- its tail (the slowest instances of the last waves, then the general
-    kernel over its bailed ones: 2.5 % + 1 % of a 2^23-instance step,
-    tools/ev_wave_times.py) overlaps the next step's work instead of idling
-    the GPU.  All K steps still complete inside the timed region."""
+    asynchronous, timed with an event pair.  Steps of up to 2^24 instances
+    alternate between two HIP streams with their own output buffers (double
+    buffering): the per-lane kernel is persistent (its grid is the resident
+    capacity), so step k + 1's waves are dispatched onto the CUs that step k's
+    last waves free up -- its tail (the slowest instances of the last waves,
+    then the general kernel over its bailed ones: 2.5 % + 1 % of a
+    2^23-instance step, tools/ev_wave_times.py) overlaps the next step's work.
+    Larger steps use one stream: there the overlapped launches slow each other
+    (the general kernel co-runs with the next per-lane kernel at a fraction
+    of its speed, and the 1-block finalize behind it waits for that kernel to
+    end), MI355X A/B (profiles/r04_notes/wave_times.txt): 2^23 +1.9 %, 2^24
+    +0.4 %, 2^25 +-0, 2^26 -0.7 % for two streams.  All K steps complete
+    inside the timed region either way."""
 
     def __init__(self, cfg, n, rank, world, stream, dev, outputs=True):
         import torch
         import pxb
         self.torch, self.pxb = torch, pxb
         self.cfg, self.n, self.rank, self.world, self.stream, self.dev = cfg, n, rank, world, stream, dev
-        self.streams = [stream, stream if ONE_STREAM else torch.cuda.Stream(dev)]
+        ns = STEP_STREAMS or (2 if n <= (1 << 24) else 1)
+        self.streams = [stream] + [torch.cuda.Stream(dev) for _ in range(ns - 1)]
+        ns = len(self.streams)
         # (outputs=False: run totals only, no per-instance records)
-        self.out = [torch.empty((n, 4), dtype=torch.int32, device=dev) if outputs else None for _ in range(2)]
+        self.out = [torch.empty((n, 4), dtype=torch.int32, device=dev) if outputs else None for _ in range(ns)]
         self.dig = [torch.empty((n, cfg.n_acceptors), dtype=torch.int32, device=dev) if outputs else None
-                    for _ in range(2)]
+                    for _ in range(ns)]
         self.tot = torch.zeros(16, dtype=torch.int64, device=dev)
         self.e0 = torch.cuda.Event(enable_timing=True)
         self.e1 = torch.cuda.Event(enable_timing=True)
 
     def launch(self, step, count):
         first = (step * self.world + self.rank) * self.n      # fresh global instance ids per step/rank
-        k = step & 1
+        k = step % len(self.streams)
         st = self.streams[k]
         with self.torch.cuda.stream(st):
             self.pxb.run_device(self.cfg, first, count, d_results=self.out[k], d_digests=self.dig[k],
@@ -144,15 +152,17 @@ class GpuLeg:
         self.torch.cuda.synchronize()
 
     def mark(self, which):
-        # (e1 - e0) / K is the mean step time over both streams, gaps between kernels included
-        a, b = self.streams
+        # (e1 - e0) / K is the mean step time over all step streams, gaps between kernels included
+        a = self.streams[0]
         if which == 0:
             self.e0.record(a)
-            b.wait_event(self.e0)
+            for b in self.streams[1:]:
+                b.wait_event(self.e0)
         else:
-            done_b = self.torch.cuda.Event()
-            done_b.record(b)
-            a.wait_event(done_b)
+            for b in self.streams[1:]:
+                done_b = self.torch.cuda.Event()
+                done_b.record(b)
+                a.wait_event(done_b)
             self.e1.record(a)
 
     def event_ms(self):
@@ -192,7 +202,7 @@ def run_workload(leg, n, steps, warmup, world, warm_n=None):
     from the leg's events; run totals summed over ranks)."""
     import torch
     import torch.distributed as dist
-    if hasattr(leg, "prime") and warmup < 2:    # (two warmup steps touch both streams)
+    if hasattr(leg, "prime") and warmup < len(getattr(leg, "streams", ())):   # (else the warmup touches every stream)
         leg.prime()
     for w in range(warmup):
         leg.launch(w, warm_n or n)
@@ -461,8 +471,8 @@ def main():
     import torch.distributed as dist
     if args.dry_run:
         return dry_main(args, rank, world)
-    global ONE_STREAM
-    ONE_STREAM = args.one_stream
+    global STEP_STREAMS
+    STEP_STREAMS = 1 if args.one_stream else args.streams
     import pxb
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
