@@ -107,11 +107,13 @@ class GpuLeg:
     last waves free up -- its tail (the slowest instances of the last waves,
     then the general kernel over its bailed ones: 2.5 % + 1 % of a
     2^23-instance step, tools/ev_wave_times.py) overlaps the next step's work.
-    Larger steps use one stream: there the overlapped launches slow each other
+    Larger faulty steps use one stream: there the overlapped launches slow each other
     (the general kernel co-runs with the next per-lane kernel at a fraction
     of its speed, and the 1-block finalize behind it waits for that kernel to
     end), MI355X A/B (profiles/r04_notes/wave_times.txt): 2^23 +1.9 %, 2^24
-    +0.4 %, 2^25 +-0, 2^26 -0.7 % for two streams.  All K steps complete
+    +0.4 %, 2^25 +-0, 2^26 -0.7 % for two streams.  Fault-free batches (config 2:
+    the fault-free per-lane kernel, not persistent) keep two streams at any
+    size: 2^28 per step, 4.3 ms with two against 5.4 ms alone.  All K steps complete
     inside the timed region either way."""
 
     def __init__(self, cfg, n, rank, world, stream, dev, outputs=True):
@@ -119,7 +121,8 @@ class GpuLeg:
         import pxb
         self.torch, self.pxb = torch, pxb
         self.cfg, self.n, self.rank, self.world, self.stream, self.dev = cfg, n, rank, world, stream, dev
-        ns = STEP_STREAMS or (2 if n <= (1 << 24) else 1)
+        fault_free = cfg.loss_ppm == 0 and cfg.crash_ppm == 0      # (the fault-free kernels: not persistent)
+        ns = STEP_STREAMS or (2 if (n <= (1 << 24) or fault_free) else 1)
         self.streams = [stream] + [torch.cuda.Stream(dev) for _ in range(ns - 1)]
         ns = len(self.streams)
         # (outputs=False: run totals only, no per-instance records)
