@@ -286,7 +286,7 @@ struct EvLane {
   bool pq_old;                        // the head pending broadcast was made at step s - 1
   uint32_t canon0;                    // canon on entering a step that carries one over (else canon - 1)
   pool_mask_t pfree;                  // free response-pool words
-  uint32_t lflags, rounds, dval, dtick, execs, msgs, canon;
+  uint32_t lflags, rounds, dval, dtick, execs, msgs, canon;   // (msgs: the replies; see msgs_sent)
   unsigned long long clog;            // canonical log, 2-bit values (divergence check, SEMANTICS §7)
   uint32_t clog_len;
   bool bailed;
@@ -357,7 +357,14 @@ struct EvLane {
   template <int K, int I = 0>
   __host__ __device__ static __forceinline__ void set_from(uint32_t (&v)[K], uint32_t oh, uint32_t x) {
     if constexpr (I < K) {
+#if defined(__HIP_DEVICE_COMPILE__)
+      // (the element's new value in its own register, a tied operand: LLVM
+      // otherwise gave some loop-carried elements a second register and
+      // copied them back at the loop's end)
+      __asm__("v_bfi_b32 %0, %1, %2, %0" : "+v"(v[I]) : "v"(lane_mask<I>(oh)), "v"(x));
+#else
       v[I] = bfi(lane_mask<I>(oh), x, v[I]);
+#endif
       set_from<K, I + 1>(v, oh, x);
     }
   }
@@ -606,9 +613,6 @@ struct EvLane {
     pq |= (p0 ? ((q << 3) | slot0) << (5u * pq_len) : 0u) | (p1 ? ((q << 3) | slot1) << (5u * pq_len + 5u) : 0u);
     const uint32_t nb = (p0 ? 1u : 0u) + (p1 ? 1u : 0u);
     pq_len += nb;
-    // every copy is counted here: an instance ends (quiet or at the step cap)
-    // only with no broadcast left to send (end_op)
-    msgs += nb * (uint32_t)N;
     put(bnext, q, (slot0 + nb) & (S::BR - 1u));
   }
 
@@ -1027,6 +1031,17 @@ struct EvLane {
       enter((int32_t)nx);
     }
     return false;
+  }
+
+  // messages sent by an ended instance: its replies plus N copies of every
+  // broadcast, counted from nsent (an instance ends -- quiet or at the step
+  // cap -- only with no broadcast left to send, end_op, so every broadcast
+  // has sent its last copy and bumped nsent)
+  __host__ __device__ __forceinline__ uint32_t msgs_sent() const {
+    uint32_t b = 0u;
+#pragma unroll
+    for (int p = 0; p < PM; ++p) b += nsent[p];
+    return msgs + b * (uint32_t)N;
   }
 
   // ---- outputs of an ended instance (SEMANTICS §7) ----

@@ -239,7 +239,7 @@ __global__ __launch_bounds__(64, CMP ? 3 : SL ? 2 : 1) void paxos_ev_kernel(EvKP
         tot.c[5] += (f & PXB_F_STEP_CAP) ? 1u : 0u;
         tot.c[6] += L.rounds;
         tot.c[7] += o.steps;
-        tot.c[8] += L.msgs;
+        tot.c[8] += L.msgs_sent();
         tot.c[9] += L.execs;
         if (LG) tot.c[10] += (f & PXB_F_LOG_TRUNC) ? 1u : 0u;
         tot.canon += L.canon;

@@ -112,7 +112,7 @@ int run_shape(const pxb_config* cfg, pxb_result* out, uint32_t* dig, pxb_accepto
         tot[PXB_C_STEP_CAP] += !!(f & PXB_F_STEP_CAP);
         tot[PXB_C_ROUNDS] += L.rounds;
         tot[PXB_C_STEPS] += o.steps;
-        tot[PXB_C_MESSAGES] += L.msgs;
+        tot[PXB_C_MESSAGES] += L.msgs_sent();
         tot[PXB_C_EXECUTES] += L.execs;
         tot[PXB_C_LOG_TRUNC] += !!(f & PXB_F_LOG_TRUNC);
         tot[PXB_C_CANON_BYTES] += L.canon;
