@@ -812,3 +812,20 @@ def test_step_kats_on_gpu(gpu_lib, case, production):
         assert [[int(x) for x in p[:4]] for p in r["prop"]] == cp["prop"], cp["step"]
         if "in_flight" in cp and r["in_flight"] != pxb.TRACE_IN_FLIGHT_UNKNOWN:
             assert r["in_flight"] == cp["in_flight"], cp["step"]
+
+
+@pytest.mark.parametrize("kind", ["simple", "compact", "split", "log"])
+def test_fuzz_per_lane_shapes(gpu_lib, kind):
+    """A slice of tests/fuzz_gpu.py in the suite: 12 schedules per per-lane
+    shape family (the simple schedule of BASELINE config 4, the compact
+    layouts, the fuzzed-P split, faulty log mode) x 2048 instances, GPU
+    against the oracle instance by instance and in the run totals."""
+    import fuzz_gpu
+    rng = np.random.default_rng({"simple": 11, "compact": 12, "split": 13, "log": 14}[kind])
+    for _ in range(12):
+        cfg = fuzz_gpu.draw(rng, kind)
+        first = int(rng.integers(0, 1 << 40))
+        res, dig, _, cnt = pxb.run(cfg, first, 2048)
+        eres, edig, _, ecnt = oracle_c.run_cpu(cfg, first, 2048, threads=THREADS)
+        assert np.array_equal(res, eres) and np.array_equal(dig, edig), cfg
+        assert cnt == ecnt, cfg
