@@ -112,6 +112,14 @@ int run_shape(const pxb_config* cfg, pxb_result* out, uint32_t* dig, pxb_accepto
         tot[PXB_C_STEP_CAP] += !!(f & PXB_F_STEP_CAP);
         tot[PXB_C_ROUNDS] += L.rounds;
         tot[PXB_C_STEPS] += o.steps;
+#ifdef PXB_HOST_CHECKED
+        // msgs_sent() counts N copies of every broadcast from nsent: an ended
+        // instance has no broadcast left to send
+        if (L.pq_len != 0u) {
+          fprintf(stderr, "ev_host: instance ended with %u pending broadcasts\n", L.pq_len);
+          abort();
+        }
+#endif
         tot[PXB_C_MESSAGES] += L.msgs_sent();
         tot[PXB_C_EXECUTES] += L.execs;
         tot[PXB_C_LOG_TRUNC] += !!(f & PXB_F_LOG_TRUNC);
