@@ -99,10 +99,13 @@ constexpr uint32_t Q_GEN = 0, Q_EV = 1, Q_BAIL = 2, Q_EV2 = 3, Q_BAIL2 = 4;
 // thread t reads column t % 16 of rows t/16, t/16+16, ...
 __global__ __launch_bounds__(TCOPIES) void finalize_kernel(unsigned long long* part, unsigned long long* part_ev,
                                                             uint32_t* queue, uint32_t bail_word, uint32_t bail_cap,
-                                                            unsigned long long* totals) {
+                                                            unsigned long long* totals, unsigned long long* hand) {
   __shared__ unsigned long long acc[16];
   const uint32_t t = threadIdx.x;
   if (t < 16) acc[t] = 0ull;
+  // the device's hand-off counts (pxb_handoff_counts): instances the first
+  // per-lane kernel handed on, and those a second one handed on
+  if (t < 2 && queue[t ? Q_BAIL2 : Q_BAIL]) atomicAdd(&hand[t], (unsigned long long)queue[t ? Q_BAIL2 : Q_BAIL]);
   __syncthreads();
   const bool ev_ok = queue[bail_word] <= bail_cap;
   unsigned long long v = 0ull;
@@ -122,7 +125,7 @@ __global__ __launch_bounds__(TCOPIES) void finalize_kernel(unsigned long long* p
 typedef void (*kernel_ptr)(KParams);
 typedef void (*ev_kernel_ptr)(ev::EvKParams);
 
-template <int PM, int W, bool C, bool L = false, bool S = false, bool SP = false>
+template <int PM, int W, bool C, bool L = false, bool S = false, int SP = 0>
 static ev_kernel_ptr ev_pick_n(uint32_t n) {
   switch (n) {
     case 2: return ev::paxos_ev_kernel<PM, 2, W, C, L, S, SP>;
@@ -173,7 +176,8 @@ static ffp_kernel_ptr ffp_pick(uint32_t p, uint32_t n) {
 
 // layout index: 0 = 8-step wheel, 1 = 16-step wheel, 2 / 3 = compact links (8- / 4-step wheel),
 // 4 = log mode (8-step wheel), 5 = slim (8-step wheel, byte reply seqs), 6 = layout 3 for
-// simple schedules (no loss, no Tick skew: ev::layout_for)
+// simple schedules (no loss, no Tick skew: ev::layout_for), 7 = layout 6 with halfword
+// response FIFOs (tight: the first launch of the two-proposer simple schedules, P = 2 only)
 static ev_kernel_ptr ev_pick(uint32_t pm, uint32_t n, int layout) {
   switch (pm * 10 + (uint32_t)layout) {
     case 10: return ev_pick_n<1, 8, false>(n);
@@ -182,21 +186,22 @@ static ev_kernel_ptr ev_pick(uint32_t pm, uint32_t n, int layout) {
     case 13: return ev_pick_n<1, 4, true>(n);
     case 14: return ev_pick_n<1, 8, false, true>(n);
     case 15: return ev_pick_n<1, 8, false, false, true>(n);
-    case 16: return ev_pick_n<1, 4, true, false, false, true>(n);
+    case 16: return ev_pick_n<1, 4, true, false, false, 1>(n);
     case 20: return ev_pick_n<2, 8, false>(n);
     case 21: return ev_pick_n<2, 16, false>(n);
     case 22: return ev_pick_n<2, 8, true>(n);
     case 23: return ev_pick_n<2, 4, true>(n);
     case 24: return ev_pick_n<2, 8, false, true>(n);
     case 25: return ev_pick_n<2, 8, false, false, true>(n);
-    case 26: return ev_pick_n<2, 4, true, false, false, true>(n);
+    case 26: return ev_pick_n<2, 4, true, false, false, 1>(n);
+    case 27: return ev_pick_n<2, 4, true, false, false, 2>(n);
     case 30: return ev_pick_n<3, 8, false>(n);
     case 31: return ev_pick_n<3, 16, false>(n);
     case 32: return ev_pick_n<3, 8, true>(n);
     case 33: return ev_pick_n<3, 4, true>(n);
     case 34: return ev_pick_n<3, 8, false, true>(n);
     case 35: return ev_pick_n<3, 8, false, false, true>(n);
-    case 36: return ev_pick_n<3, 4, true, false, false, true>(n);
+    case 36: return ev_pick_n<3, 4, true, false, false, 1>(n);
   }
   return nullptr;
 }
@@ -257,6 +262,8 @@ static int g_cus[64];
 constexpr int QSLOTS = 64;
 constexpr size_t ROWS_U64 = (size_t)TCOPIES * 16;
 constexpr size_t SLOT_U64 = 2 * ROWS_U64 + 16;
+// (+ 16 words after the last slot: the device's hand-off counts)
+constexpr size_t HAND_U64 = (size_t)QSLOTS * SLOT_U64;
 static unsigned long long* g_slots[64];
 static uint32_t g_qseq[64];
 // Per-lane kernel: one launch per EV_CHUNK instances; its bailed ids go to a
@@ -295,7 +302,7 @@ struct EvLists {
 };
 static EvLists g_lists[64][EV_LIST_STREAMS];
 static int g_nlists[64], g_lnext[64];
-static int g_eocc[7][4][10][64];
+static int g_eocc[8][4][10][64];
 static int g_ff1occ[10][64];
 static int g_ffpocc[4][10][64];
 
@@ -404,8 +411,8 @@ extern "C" void pxb_stream_release(int dev, void* stream) {
 static int ensure_slots(int dev) {
   if (g_slots[dev]) return PXB_OK;
   unsigned long long* q = nullptr;
-  HIPCHK(hipMalloc(&q, QSLOTS * SLOT_U64 * sizeof(unsigned long long)));
-  HIPCHK(hipMemset(q, 0, QSLOTS * SLOT_U64 * sizeof(unsigned long long)));
+  HIPCHK(hipMalloc(&q, (HAND_U64 + 16) * sizeof(unsigned long long)));
+  HIPCHK(hipMemset(q, 0, (HAND_U64 + 16) * sizeof(unsigned long long)));
   HIPCHK(hipDeviceSynchronize());
   g_slots[dev] = q;
   return PXB_OK;
@@ -480,6 +487,24 @@ const char* pxb_strerror(int code) {
 
 uint64_t pxb_canonical_bytes_nofault(uint32_t n_acceptors) { return 196ull * n_acceptors + 160ull; }
 
+int pxb_handoff_counts(int dev, uint64_t* out2, int reset) {
+  if (!out2 || dev < 0 || dev >= 64) return PXB_E_INVAL;
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_slots[dev]) {
+    out2[0] = out2[1] = 0;
+    return PXB_OK;
+  }
+  int cur = 0;
+  HIPCHK(hipGetDevice(&cur));
+  HIPCHK(hipSetDevice(dev));
+  unsigned long long* h = g_slots[dev] + HAND_U64;
+  hipError_t e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpy(out2, h, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost);
+  if (e == hipSuccess && reset) e = hipMemset(h, 0, 2 * sizeof(uint64_t));
+  (void)hipSetDevice(cur);
+  return e == hipSuccess ? PXB_OK : hip_fail(e);
+}
+
 int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_digest,
                    pxb_acceptor_rec* d_acc, int64_t* d_totals, void* stream) {
   int rc = validate(cfg);
@@ -534,7 +559,18 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
   const char* no_split = getenv("PXB_NO_SPLIT");
   const bool may_split = use_ev && (cfg->flags & PXB_CFG_RANDOMIZE) && cfg->n_proposers == 3 &&
                          !(no_split && atoi(no_split) > 0);
-  const ev_kernel_ptr sfn = may_split ? ev_pick(2, cfg->n_acceptors, layout) : nullptr;
+  // Tight routing of two-proposer simple schedules whose layout-6 lane takes
+  // more than 52 LDS words (config 4: 60 words, 10 waves per CU, so half the
+  // SIMDs run 2 waves and half 3): layout 7 (52 words, 12 waves per CU)
+  // runs over the chunk first and lists its bails (config 4: 0.5 %, nearly all
+  // a full 3-deep response FIFO) for layout 6 over that list, whose own bails
+  // go to the general kernel.  PXB_NO_TIGHT=1 turns it off.
+  const char* no_tight = getenv("PXB_NO_TIGHT");
+  const bool may_tight = use_ev && layout == 6 && cfg->n_proposers == 2 && cfg->n_proposers * cfg->n_acceptors > 10 &&
+                         !(no_tight && atoi(no_tight) > 0);
+  const ev_kernel_ptr sfn = may_split ? ev_pick(2, cfg->n_acceptors, layout)
+                            : may_tight ? ev_pick(2, cfg->n_acceptors, 7) : nullptr;
+  // (split: the two-stage routing of either kind)
   bool split = false;
   const hipStream_t st = (hipStream_t)stream;
   int occ, cus, eocc = 0, socc = 0;
@@ -557,8 +593,8 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
     const int target = 4 * fn.occ;
     occ = std::min(o, std::max(1, target / fn.wpb));   // blocks per CU
     cus = g_cus[dev];
-    auto ev_occ = [&](ev_kernel_ptr k, uint32_t pm, int* out) -> int {
-      int& eo = g_eocc[layout][pm][cfg->n_acceptors][dev];
+    auto ev_occ = [&](ev_kernel_ptr k, uint32_t pm, int lay, int* out) -> int {
+      int& eo = g_eocc[lay][pm][cfg->n_acceptors][dev];
       if (!eo) {
         int nb = 0;
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)k, 64, 0));
@@ -586,9 +622,9 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
       eocc = fo;
     }
     if (use_ev) {
-      if (int rc2 = ev_occ(efn, cfg->n_proposers, &eocc)) return rc2;
+      if (int rc2 = ev_occ(efn, cfg->n_proposers, layout, &eocc)) return rc2;
       if (sfn) {
-        if (int rc2 = ev_occ(sfn, 2, &socc)) return rc2;
+        if (int rc2 = ev_occ(sfn, 2, may_tight ? 7 : layout, &socc)) return rc2;
         split = socc > eocc;
       }
     }
@@ -640,7 +676,8 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
   const uint64_t wpb = (uint64_t)fn.wpb;
   // fault-free log mode: 16-bit epochs, so every block's range (static slices:
   // every wave's) stays below 2^16 instances
-  const uint64_t ev_chunk = split ? EV_SPLIT_CHUNK : EV_CHUNK;
+  // (tight: bails are rare, so whole chunks; the list holds a quarter of one)
+  const uint64_t ev_chunk = (split && !may_tight) ? EV_SPLIT_CHUNK : EV_CHUNK;
   // fault-free per-lane kernels: as few launches as the general faulty kernel
   // allows (it may have to re-run a whole chunk); A/B on config 2 at 2^26:
   // 2^24-instance launches 2 % slower, 2^22 10 %, 2^20 33 %
@@ -739,7 +776,9 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
     } else if (use_ev) {
       // the per-lane kernel over the chunk, then the general kernel over its
       // bailed ids; split: the two-proposer shape over the chunk, the
-      // three-proposer shape over its list, the general kernel over that one's
+      // three-proposer shape over its list, the general kernel over that one's;
+      // tight: layout 7 over the chunk, layout 6 over its list, the general
+      // kernel over that one's
       ev::EvKParams ek;
       memset(&ek, 0, sizeof(ek));
       ek.p = ev::make_params(cfg);
@@ -758,6 +797,11 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
         sk.bail_ids = slist;
         sk.bail_cap = std::min<uint32_t>(bail_cap == EV_BAIL_CAP ? EV_SPLIT_CAP : bail_cap, EV_SPLIT_CAP);
         const unsigned sgrid = (unsigned)std::min<uint64_t>((nc + 63) / 64, (uint64_t)socc * (uint64_t)cus);
+#ifdef PXB_WAVE_TIMES   // (two-stage: the first per-lane launch's timeline)
+        if (!g_wt) HIPCHK(hipMalloc(&g_wt, 6ull * 65536 * sizeof(unsigned long long)));
+        sk.dbg = g_wt;
+        g_wt_waves = sgrid;
+#endif
         hipLaunchKernelGGL(sfn, dim3(sgrid), dim3(64), 0, st, sk);
         HIPCHK(hipGetLastError());
         ek.ids = slist;
@@ -771,8 +815,8 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
       const unsigned egrid = (unsigned)std::min<uint64_t>((nc + 63) / 64, eres);
 #ifdef PXB_WAVE_TIMES
       if (!g_wt) HIPCHK(hipMalloc(&g_wt, 6ull * 65536 * sizeof(unsigned long long)));
-      ek.dbg = g_wt;
-      g_wt_waves = egrid;
+      ek.dbg = split ? nullptr : g_wt;
+      if (!split) g_wt_waves = egrid;
 #endif
       hipLaunchKernelGGL(efn, dim3(egrid), dim3(64), 0, st, ek);
       if (hipError_t e = hipGetLastError()) return fail(e);
@@ -795,7 +839,7 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
       HIPCHK(hipGetLastError());
     }
     hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(TCOPIES), 0, st, kp.part, kp.part + ROWS_U64, kp.queue,
-                       bail_word, bail_cap, totals);
+                       bail_word, bail_cap, totals, g_slots[dev] + HAND_U64);
     if (hipError_t e = hipGetLastError()) return fail(e);
     if (lent)
       if (int rc2 = list_used(lent, st)) return rc2;

@@ -69,10 +69,15 @@ static_assert(MAX_STEP_CAP < PXB_TICKET_LIMIT, "EV tickets never reach the overf
 // lane modes
 constexpr uint32_t M_IDLE = 0, M_RUN = 1;
 
-template <int PM_, int N_, int POOL_, int W_, bool CMP_, bool LG_ = false, bool SL_ = false, bool SP_ = false>
+template <int PM_, int N_, int POOL_, int W_, bool CMP_, bool LG_ = false, bool SL_ = false, int SP_ = 0>
 struct Shape {
   static constexpr int PM = PM_, N = N_, POOL = POOL_, W = W_;
-  static constexpr bool SP = SP_;                    // simple schedule: no loss, no Tick skew, single decree
+  static constexpr bool SP = SP_ != 0;               // simple schedule: no loss, no Tick skew, single decree
+  // tight (SP_ == 2, layout 7): the simple schedule's compact layout with the
+  // response FIFOs in halfwords (3 entries of pool index + 1 or a Round2Success
+  // code, zero above the length), so that a lane fits 52 LDS words (13 KB per
+  // wave: 12 waves per CU, 3 on every SIMD); its bails re-run on layout 6
+  static constexpr bool RH = SP_ == 2;
   static constexpr bool CMP = CMP_;                  // compact links (see Layouts)
   static constexpr bool LG = LG_;                    // log mode (several Ticks, long logs; see Layouts)
   static constexpr bool SL = SL_;                    // slim 4-entry layout (see Layouts)
@@ -100,8 +105,12 @@ struct Shape {
   // +28 ms (it now runs those long instances itself): +0.7 % end to end.  On the
   // two-proposer shape (0.01 % bails) it only costs (-1 %): not used there.
   static constexpr bool RSN = SL && PM * N > 18;
-  static constexpr int RC = RSN ? 5 : 4, RL = IB * RC, RLB = 3, RD = RL + RLB;
-  static constexpr int POOLB_SHIFT = RSN ? 1 : 0;    // entry e's pool word: POOLW - POOLB_SHIFT + e
+  // (RZ: entries are pool index + 1, zero above the length, the length from
+  // the highest set bit and the tail's due from its pool word or code)
+  static constexpr bool RZ = RSN || RH;
+
+  static constexpr int RC = RH ? 3 : RSN ? 5 : 4, RL = IB * RC, RLB = 3, RD = RL + RLB;
+  static constexpr int POOLB_SHIFT = RZ ? 1 : 0;     // entry e's pool word: POOLW - POOLB_SHIFT + e
   // compact layouts with a pool of <= 24 words: a Round2Success (no payload)
   // takes no pool word; its FIFO entry is the code RCB + (due & 7) instead
 #ifdef PXB_EV_NO_RCODE
@@ -115,7 +124,7 @@ struct Shape {
   static constexpr int RSEQ = REQ + NLQ;             // !CMP: NLQ halfwords of reply seq, index a*PM + p
   // (slim: the reply seqs are bytes in registers)
   static constexpr int RSP = RSEQ + ((CMP || SL) ? 0 : (NLQ + 1) / 2);   // NLQ response links, index p*N + a
-  static constexpr int POOLW = RSP + NLQ;            // POOL response words
+  static constexpr int POOLW = RSP + (RH ? (NLQ + 1) / 2 : NLQ);   // POOL response words (RH: links in halfwords)
   // broadcast ring slots per proposer: short-delay (compact) schedules never
   // hold more than 4 broadcasts of one proposer in flight (BASELINE configs
   // 3 and 4: the bail rate is the same with 4 slots as with 8), nor does
@@ -131,7 +140,11 @@ struct Shape {
   static constexpr int WORDS = WHEEL + W * WW;
   static_assert(W == 4 || W == 8 || W == 16, "wheel of 4, 8 or 16 steps");
   static_assert(NIN <= 32 && NLQ <= 32, "masks are 32-bit");
-  static_assert(RSN ? (IB * RC <= 32 && POOL < (1 << IB)) : (RD + 4 <= 32), "response-link word");
+  static_assert(RH ? (IB * RC <= 16 && CMP && W == 4) : RSN ? (IB * RC <= 32 && POOL < (1 << IB)) : (RD + 4 <= 32),
+                "response-link word");
+  // (index + 1 below the Round2Success codes)
+  static_assert(!(RZ && RCODE) || POOL < (int)RCB, "pool entries and codes");
+  static_assert(!RH || (SP && !LG && RCODE && DB == 3), "layout 7: simple single decree, 4-step wheel");
   static constexpr int POOLB = POOLW - POOLB_SHIFT;
   static_assert(QL + QLB <= 31, "request-link word");
 };
@@ -230,7 +243,7 @@ struct EvOut {
 // (see end_op); the trace kernel turns it off so that its per-step records
 // hold every message of the step in flight, as the oracle's do.
 template <int PM, int N, int POOL, int W, bool CMP, class Mem, bool EARLY = true, bool LG = false, bool SL = false,
-          bool SP = false>
+          int SP = 0>
 struct EvLane {
   using S = Shape<PM, N, POOL, W, CMP, LG, SL, SP>;
   // acceptor fields (Layouts): dead bit, log-length shift (LG: in accv) and its limit
@@ -411,8 +424,13 @@ struct EvLane {
     if (PM == 2) return q;
     return slot & 1u;
   }
-  __host__ __device__ __forceinline__ uint32_t rsp_ld(uint32_t Lr) const { return m.ld(S::RSP + Lr); }
-  __host__ __device__ __forceinline__ void rsp_st(uint32_t Lr, uint32_t v) const { m.st(S::RSP + Lr, v); }
+  __host__ __device__ __forceinline__ uint32_t rsp_ld(uint32_t Lr) const {
+    return S::RH ? m.ldh(S::RSP, Lr) : m.ld(S::RSP + Lr);
+  }
+  __host__ __device__ __forceinline__ void rsp_st(uint32_t Lr, uint32_t v) const {
+    if constexpr (S::RH) m.sth(S::RSP, Lr, v);
+    else m.st(S::RSP + Lr, v);
+  }
 
   // the Tick bits of step t
   __host__ __device__ __forceinline__ uint32_t ticks_at(int32_t t) const {
@@ -545,7 +563,11 @@ struct EvLane {
       accd[a] = 0x811C9DC5u;
     }
 #pragma unroll
-    for (int i = S::REQ; i < S::POOLW; ++i) m.st(i, 0u);     // request links, reply seqs, response links
+    for (int i = S::REQ; i < (S::RH ? S::RSP : S::POOLW); ++i) m.st(i, 0u);   // request links, reply seqs, response links
+    if constexpr (S::RH) {                           // (halfword rows shared with the other lanes' words)
+#pragma unroll
+      for (int i = 0; i < NLQ; ++i) m.sth(S::RSP, i, 1u);   // empty: the sentinel
+    }
     if constexpr (SL) {
 #pragma unroll
       for (int i = 0; i < (int)((NLQ + 3) / 4); ++i) rseqv[i] = 0u;
@@ -656,46 +678,88 @@ struct EvLane {
     const uint32_t base = isR ? (uint32_t)s : sb;   // the send step (a carried copy's is s - 1)
     const uint32_t b4 = base & 15u;
     const uint32_t Lq = ca * (uint32_t)PM + cp;
-    const uint32_t lw = isR ? S::RSP + rp.Lr : S::REQ + Lq;   // the link word
-    const uint32_t wv = m.ld(lw);
-    uint32_t rlen, rtail;
-    if constexpr (S::RSN) {                          // (the tail entry's pool word holds its due)
-      rlen = (nbits32(wv) + (uint32_t)S::IB - 1u) / (uint32_t)S::IB;
-      const uint32_t te = (wv >> ((S::IB * rlen - S::IB) & 31u)) & (isR ? IM : 0u);
-      rtail = (m.ld(S::POOLB + te) >> 26) & 15u;
-    } else {
-      rlen = (wv >> S::RL) & RLM;
-      rtail = (wv >> S::RD) & 15u;
-    }
-    const uint32_t len = isR ? rlen : (wv >> S::QL) & QLM;
-    // (a request entry's due is mod 2^DB: every queued due lies within 2^DB of the send step)
-    const uint32_t tail = isR ? rtail : (wv >> (((uint32_t)S::EB * len - (uint32_t)S::DB) & 31u)) & DM;
-    const uint32_t rel = (tail - b4) & (len ? (isR ? 15u : DM) : 0u);
-    const uint32_t due_rel = d > rel ? d : rel;
-    const uint32_t due4 = (b4 + due_rel) & 15u;
     // (a Round2Success in a compact link word needs no pool word)
     const bool r2c = S::RCODE & isR & ((rp.pw >> 30) == R2S);
-    bailed = bailed | (go & (isR ? (len >= (uint32_t)S::RC) | ((pfree == 0) & !r2c) : (len >= (uint32_t)S::QC)));
-    PXB_EV_PROBE(EVB_RFIFO, go & isR & (len >= (uint32_t)S::RC));
-    PXB_EV_PROBE(EVB_POOL, go & isR & (pfree == 0) & !r2c);
-    PXB_EV_PROBE(EVB_QFIFO, go & !isR & (len >= (uint32_t)S::QC));
     const uint32_t k2 = (POOL > 32) ? (uint32_t)__builtin_ctzll((unsigned long long)pfree | (1ull << 63))
                                     : ctz32((uint32_t)pfree) & 31u;
-    // the pool word: to a free entry (harmless unless a reply goes), or, with
-    // none free, to the link word, which the next store rewrites
-    m.st(pfree ? S::POOLB + k2 : lw, rp.pw | (due4 << 26));
-    if constexpr (LG) {                              // (no free entry: the dummy halfword)
-      const uint32_t zi = pfree ? k2 : (uint32_t)POOL;
-      m.st16h(S::POOLZ + (zi >> 1), zi & 1u, rp.z);
+    uint32_t due_rel, due4;
+    if constexpr (S::RH) {
+      // Halfword response links (layout 7): both link words are loaded (the
+      // request word of the copy, the response halfword of the reply) and
+      // both are stored back, so no halfword is extracted from a shared word.
+      // A response halfword holds its entries (pool index + 1, or a
+      // Round2Success code) from bit 0 and a sentinel bit above the last
+      // (empty: 1), so its highest set bit gives the tail's offset (+ 5)
+      // and the append position.
+      const uint32_t wq = m.ld(S::REQ + Lq);
+      const uint32_t h = rsp_ld(rp.Lr);
+      const uint32_t msb = 31u - (uint32_t)__builtin_clz(h | 1u);   // (h >= 1: the sentinel)
+      const uint32_t te = (h >> ((msb - (uint32_t)S::IB) & 31u)) & IM;   // (empty: >> 27 = 0)
+      // (a Round2Success code carries its due & 7; a code's or an empty link's pool load is unused)
+      const uint32_t tp = (m.ld(S::POOLB + te) >> 26) & 15u;
+      const uint32_t rtail = (te >= S::RCB) ? te & 7u : tp;
+      const uint32_t qlen = (wq >> S::QL) & QLM;
+      const uint32_t qtail = (wq >> (((uint32_t)S::EB * qlen - (uint32_t)S::DB) & 31u)) & DM;
+      const uint32_t nz = isR ? h - 1u : qlen;           // (0: the link is empty)
+      const uint32_t rel = ((isR ? rtail : qtail) - b4) & (nz ? 7u : 0u);   // (DM = 7: the 4-step wheel)
+      due_rel = d > rel ? d : rel;
+      due4 = (b4 + due_rel) & 15u;
+      const bool rfull = h >= (1u << (S::IB * S::RC));
+      // (as integers: a select of two booleans became five instructions)
+      const uint32_t pool_out = (pfree == 0) & !r2c ? 1u : 0u;
+      const uint32_t full = isR ? (h >> (S::IB * S::RC)) | pool_out : qlen >> 2;   // (QC = 4, qlen <= 4)
+      static_assert(S::QC == 4, "request FIFOs of 4");
+      bailed = bailed | (go & (full != 0u));
+      PXB_EV_PROBE(EVB_RFIFO, go & isR & rfull);
+      PXB_EV_PROBE(EVB_POOL, go & isR & (pfree == 0) & !r2c);
+      PXB_EV_PROBE(EVB_QFIFO, go & !isR & (qlen >= (uint32_t)S::QC));
+      // the pool word: to a free entry (harmless unless a reply goes), or, with
+      // none free, to the request word, which the next store rewrites
+      m.st(pfree ? S::POOLB + k2 : S::REQ + Lq, rp.pw | (due4 << 26));
+      const uint32_t ent = r2c ? S::RCB + (due4 & 7u) : k2;
+      // (the entry replaces the sentinel, the sentinel moves up one entry)
+      const uint32_t nR = h + ((ent + (1u << S::IB) - 1u) << msb);
+      const uint32_t nQ = wq + (1u << S::QL) + ((cslot | ((due4 & DM) << S::SB)) << ((uint32_t)S::EB * qlen));
+      m.st(S::REQ + Lq, (go & !isR) ? nQ : wq);
+      rsp_st(rp.Lr, (go & isR) ? nR : h);
+    } else {
+      const uint32_t lw = isR ? S::RSP + rp.Lr : S::REQ + Lq;   // the link word
+      const uint32_t wv = m.ld(lw);
+      uint32_t rlen, rtail;
+      if constexpr (S::RZ) {                         // (the tail entry's pool word holds its due)
+        rlen = (nbits32(wv) + (uint32_t)S::IB - 1u) / (uint32_t)S::IB;
+        const uint32_t te = (wv >> ((S::IB * rlen - S::IB) & 31u)) & (isR ? IM : 0u);
+        rtail = (m.ld(S::POOLB + te) >> 26) & 15u;
+      } else {
+        rlen = (wv >> S::RL) & RLM;
+        rtail = (wv >> S::RD) & 15u;
+      }
+      const uint32_t len = isR ? rlen : (wv >> S::QL) & QLM;
+      // (a request entry's due is mod 2^DB: every queued due lies within 2^DB of the send step)
+      const uint32_t tail = isR ? rtail : (wv >> (((uint32_t)S::EB * len - (uint32_t)S::DB) & 31u)) & DM;
+      const uint32_t rel = (tail - b4) & (len ? (isR ? 15u : DM) : 0u);
+      due_rel = d > rel ? d : rel;
+      due4 = (b4 + due_rel) & 15u;
+      bailed = bailed | (go & (isR ? (len >= (uint32_t)S::RC) | ((pfree == 0) & !r2c) : (len >= (uint32_t)S::QC)));
+      PXB_EV_PROBE(EVB_RFIFO, go & isR & (len >= (uint32_t)S::RC));
+      PXB_EV_PROBE(EVB_POOL, go & isR & (pfree == 0) & !r2c);
+      PXB_EV_PROBE(EVB_QFIFO, go & !isR & (len >= (uint32_t)S::QC));
+      // the pool word: to a free entry (harmless unless a reply goes), or, with
+      // none free, to the link word, which the next store rewrites
+      m.st(pfree ? S::POOLB + k2 : lw, rp.pw | (due4 << 26));
+      if constexpr (LG) {                            // (no free entry: the dummy halfword)
+        const uint32_t zi = pfree ? k2 : (uint32_t)POOL;
+        m.st16h(S::POOLZ + (zi >> 1), zi & 1u, rp.z);
+      }
+      const uint32_t ent = r2c ? S::RCB + (due4 & 7u) : k2;
+      // (entries above a FIFO's length are 0: appends are additions)
+      constexpr int RD = S::RZ ? 0 : S::RD;         // (no due field in a slim >18-link word)
+      const uint32_t nR = S::RZ ? wv | (ent << ((S::IB * len) & 31u))
+                                : ((wv + (1u << S::RL) + (ent << (S::IB * len))) & ~(15u << RD)) | (due4 << RD);
+      const uint32_t nQ = wv + (1u << S::QL) + ((cslot | ((due4 & DM) << S::SB)) << ((uint32_t)S::EB * len));
+      m.st(lw, go ? (isR ? nR : nQ) : wv);
     }
     pfree &= (go & isR & !r2c) ? ~((pool_mask_t)1 << k2) : ~(pool_mask_t)0;
-    const uint32_t ent = r2c ? S::RCB + (due4 & 7u) : k2;
-    // (entries above a FIFO's length are 0: appends are additions)
-    constexpr int RD = S::RSN ? 0 : S::RD;          // (no due field in a slim >18-link word)
-    const uint32_t nR = S::RSN ? wv | (ent << ((S::IB * len) & 31u))
-                               : ((wv + (1u << S::RL) + (ent << (S::IB * len))) & ~(15u << RD)) | (due4 << RD);
-    const uint32_t nQ = wv + (1u << S::QL) + ((cslot | ((due4 & DM) << S::SB)) << ((uint32_t)S::EB * len));
-    m.st(lw, go ? (isR ? nR : nQ) : wv);
     ref_add(cp, cslot, (go & !isR) ? 1u : 0u);
     // a carried copy due now joins this step's due links, the rest the wheel
     const bool now = EARLY & !isR & (base + due_rel == (uint32_t)s);
@@ -916,6 +980,7 @@ struct EvLane {
       const uint32_t Lr = q * (uint32_t)N + (resp ? ra : 0u);
       const uint32_t rr = rsp_ld(Lr);
       const uint32_t rlen = (rr >> S::RL) & RLM;
+      // (RH: with one entry, nk is the sentinel: rkeep tests for a second entry)
       const uint32_t k = rr & IM, nk = (rr >> S::IB) & IM;
       // (a Round2Success code: no pool word, its due in the code)
       const bool kc = S::RCODE & (k >= S::RCB), nkc = S::RCODE & (nk >= S::RCB);
@@ -923,11 +988,11 @@ struct EvLane {
       const uint32_t pn = m.ld(S::POOLB + (nkc ? 0u : nk));
       const uint32_t pe = kc ? (R2S << 30) : pe0;
       pfree |= (resp & !kc) ? ((pool_mask_t)1 << k) : (pool_mask_t)0;
-      const uint32_t popped = S::RSN ? rr >> S::IB
-                                     : ((rr & ((1u << S::RL) - 1u)) >> S::IB) + ((rr & ~((1u << S::RL) - 1u)) - (1u << S::RL));
-      m.st(S::RSP + Lr, resp ? popped : rr);         // (popped: entries down one, length - 1)
+      const uint32_t popped = S::RZ ? rr >> S::IB
+                                    : ((rr & ((1u << S::RL) - 1u)) >> S::IB) + ((rr & ~((1u << S::RL) - 1u)) - (1u << S::RL));
+      rsp_st(Lr, resp ? popped : rr);                // (popped: entries down one, length - 1)
       const bool nnow = nkc ? ((nk & 7u) == (s4 & 7u)) : (((pn >> 26) & 15u) == s4);
-      const bool rkeep = resp & (S::RSN ? nk != 0u : rlen > 1u) & nnow;
+      const bool rkeep = resp & (S::RH ? rr >= (1u << (2 * S::IB)) : S::RZ ? nk != 0u : rlen > 1u) & nnow;
       in_mask = (pin & !rkeep) ? (in_mask & ~(1u << j)) : in_mask;
       const uint32_t rkind = pe >> 30, px = pe & 0xFFFu, py = (pe >> 12) & 0xFFFu;
       const uint32_t pz = LG ? m.ld16h(S::POOLZ + (k >> 1), k & 1u) : (pe >> 24) & 3u;
@@ -1065,9 +1130,10 @@ struct EvLane {
   __host__ __device__ uint32_t links_in_flight() const {
     uint32_t n = 0u;
     for (uint32_t L = 0; L < NLQ; ++L) {
-      const uint32_t rw = m.ld(S::RSP + L);
+      const uint32_t rw = rsp_ld(L);
       n += ((m.ld(S::REQ + L) >> S::QL) & QLM)
-           + (S::RSN ? (nbits32(rw) + (uint32_t)S::IB - 1u) / (uint32_t)S::IB : (rw >> S::RL) & RLM);
+           + (S::RH ? (nbits32(rw) - 1u) / (uint32_t)S::IB
+              : S::RZ ? (nbits32(rw) + (uint32_t)S::IB - 1u) / (uint32_t)S::IB : (rw >> S::RL) & RLM);
     }
     return n;
   }
@@ -1165,9 +1231,9 @@ __host__ inline int layout_for(const pxb_config* c) {
 #endif
   return 0;
 }
-__host__ inline int layout_wheel(int layout) { return layout == 1 ? 16 : (layout == 3 || layout == 6) ? 4 : 8; }
-__host__ inline bool layout_compact(int layout) { return layout == 2 || layout == 3 || layout == 6; }
-__host__ inline bool layout_simple(int layout) { return layout == 6; }
+__host__ inline int layout_wheel(int layout) { return layout == 1 ? 16 : (layout == 3 || layout == 6 || layout == 7) ? 4 : 8; }
+__host__ inline bool layout_compact(int layout) { return layout == 2 || layout == 3 || layout == 6 || layout == 7; }
+__host__ inline bool layout_simple(int layout) { return layout == 6 || layout == 7; }
 __host__ inline bool layout_log(int layout) { return layout == 4; }
 
 }  // namespace ev

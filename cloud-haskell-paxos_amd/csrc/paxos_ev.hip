@@ -2,7 +2,7 @@
 // (paxos_ev_kernel.h) for one proposer count (-DPXB_EV_P=1|2|3): 8 acceptor
 // counts x {8, 16}-step timing wheels (plus the compact-link
 // layout with the 8- and 4-step wheels, the log-mode fields on the 8-step
-// wheel, and the slim 8-step layout).  Split by P so the units build in
+// wheel, the slim 8-step layout, and the tight layout 7 for P = 2).  Split by P so the units build in
 // parallel.
 #include "paxos_ev_kernel.h"
 
@@ -20,7 +20,10 @@ PXB_EV_FOR_N(8, false, false, false, false)
 PXB_EV_FOR_N(16, false, false, false, false)
 PXB_EV_FOR_N(8, true, false, false, false)
 PXB_EV_FOR_N(4, true, false, false, false)
-PXB_EV_FOR_N(4, true, false, false, true)      // simple schedule (layout 6)
+PXB_EV_FOR_N(4, true, false, false, 1)         // simple schedule (layout 6)
+#if PXB_EV_P == 2
+PXB_EV_FOR_N(4, true, false, false, 2)         // tight simple schedule (layout 7; two proposers only)
+#endif
 PXB_EV_FOR_N(8, false, true, false, false)     // log mode
 PXB_EV_FOR_N(8, false, false, true, false)     // slim
 }  // namespace ev

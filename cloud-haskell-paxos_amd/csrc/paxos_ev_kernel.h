@@ -34,6 +34,14 @@ struct LdsMem {
   __host__ __device__ void st16h(uint32_t i, uint32_t half, uint32_t v) const {
     reinterpret_cast<uint16_t*>(w)[(i * 64u + lane) * 2u + half] = (uint16_t)v;
   }
+  // element i of a lane-interleaved halfword array at word `base`: [i][lane]
+  // (a halfword per lane and row: the address is one shift-add)
+  __host__ __device__ uint32_t ldh(uint32_t base, uint32_t i) const {
+    return reinterpret_cast<const uint16_t*>(w + base * 64u)[i * 64u + lane];
+  }
+  __host__ __device__ void sth(uint32_t base, uint32_t i, uint32_t v) const {
+    reinterpret_cast<uint16_t*>(w + base * 64u)[i * 64u + lane] = (uint16_t)v;
+  }
   // OR into a word (ds_or_b32: no read-back on the critical path)
   __device__ void orw(uint32_t i, uint32_t v) const { atomicOr(&w[i * 64u + lane], v); }
 };
@@ -77,9 +85,17 @@ struct EvKParams {
 // words), 30 those of 99.99 % of its P = 2 ones; compact over <= 10 links:
 // config 3 bails no more with 16 words than with 24, and its shape then leaves
 // LDS to spare at 12 waves per CU)
-template <int PM, int N, bool CMP, bool LG = false, bool SL = false>
+// (tight, layout 7: 21 words, 50 per lane: 12 resident waves per CU need
+// <= 50 (measured: 52-word lanes ran 11, the 12th block waited); 5-bit
+// entries of pool index + 1 beside the 8 Round2Success codes allow <= 23;
+// config 4 bails 0.76 % on it, host model)
+#ifndef PXB_EV_TIGHT_POOL
+#define PXB_EV_TIGHT_POOL 21
+#endif
+template <int PM, int N, bool CMP, bool LG = false, bool SL = false, int SP = 0>
 struct EvPool {
-  static constexpr int value = (LG && PM * N <= 10)  ? 18
+  static constexpr int value = (SP == 2)             ? PXB_EV_TIGHT_POOL
+                               : (LG && PM * N <= 10)  ? 18
                                : (CMP && PM * N <= 10) ? 16
                                : (PM * N <= 16)      ? (CMP ? PXB_EV_CMP_POOL : 32)
                                : CMP                ? 48
@@ -132,9 +148,9 @@ struct EvTotals {
 // on some SIMDs: its register budget is then 168 VGPRs, which the second
 // bound (minimum waves per SIMD) makes the compiler keep to.
 // The slim layout fits 5 or more waves per CU, 2 on some SIMDs: <= 256 VGPRs.
-template <int PM, int N, int W, bool CMP, bool LG = false, bool SL = false, bool SP = false>
+template <int PM, int N, int W, bool CMP, bool LG = false, bool SL = false, int SP = 0>
 __global__ __launch_bounds__(64, CMP ? 3 : SL ? 2 : 1) void paxos_ev_kernel(EvKParams kp) {
-  constexpr int POOL = EvPool<PM, N, CMP, LG, SL>::value;
+  constexpr int POOL = EvPool<PM, N, CMP, LG, SL, SP>::value;
   using S = Shape<PM, N, POOL, W, CMP, LG, SL, SP>;
   __shared__ uint32_t lds[S::WORDS * 64];
   const uint32_t lane = threadIdx.x;

@@ -209,6 +209,8 @@ def load(path: str = LIB_PATH):
         getattr(lib, name).restype = C.c_int
     lib.pxb_stream_release.argtypes = [C.c_int, vp]
     lib.pxb_stream_release.restype = None
+    lib.pxb_handoff_counts.argtypes = [C.c_int, vp, C.c_int]
+    lib.pxb_handoff_counts.restype = C.c_int
     _lib = lib
     return lib
 
@@ -413,6 +415,14 @@ def stream_release(dev: int, stream: int):
     """pxb_stream_release: a stream used with run_device is about to be
     destroyed; its bailed-id lists go back to the library."""
     load().pxb_stream_release(dev, C.c_void_p(stream))
+
+
+def handoff_counts(dev: int = 0, reset: bool = True):
+    """pxb_handoff_counts: (first per-lane kernel, second per-lane kernel)
+    hand-off counts of device dev since its scratch was created or last reset."""
+    out = (C.c_uint64 * 2)()
+    check(load().pxb_handoff_counts(dev, C.cast(out, C.c_void_p), 1 if reset else 0))
+    return int(out[0]), int(out[1])
 
 
 def shutdown():

@@ -26,7 +26,8 @@
 extern "C" {
 #endif
 
-#define PXB_ABI_VERSION 3   /* 3: pxb_init / pxb_shutdown, n_bytes bound on wire decode */
+#define PXB_ABI_VERSION 4   /* 3: pxb_init / pxb_shutdown, n_bytes bound on wire decode;
+                               4: pxb_stream_release, pxb_handoff_counts */
 
 /* ---- error codes ---------------------------------------------------------- */
 #define PXB_OK          0
@@ -192,7 +193,7 @@ int pxb_run_multi(const pxb_config* cfg, int n_devices, pxb_result* out, uint32_
 int pxb_init(int n_devices);
 int pxb_shutdown(void);
 
-/* pxb_stream_release: `stream` (a hipStream_t used with pxb_run_device on device
+/* pxb_stream_release (ABI 4): `stream` (a hipStream_t used with pxb_run_device on device
  * `dev`) is about to be destroyed: its bailed-id lists go back to the library
  * for the next stream, which first waits for the event behind their last
  * launches.  Optional (without it a ninth stream takes the oldest entry over);
@@ -330,6 +331,18 @@ int pxb_wire_encode_host(const pxb_msg* msgs, uint64_t count, uint32_t type, uin
                          uint64_t* nbytes);
 int pxb_wire_decode_host(const uint8_t* in, uint64_t n_bytes, const uint64_t* offsets, uint64_t count,
                          uint32_t type, pxb_msg* msgs, uint32_t* status);
+
+/* pxb_handoff_counts: instances the per-lane kernels of device `dev` handed on
+ * since the device's scratch was created (pxb_init or its first launch) or
+ * last reset: out2[0] = by the first per-lane kernel of a chunk (its bails; for
+ * the two-stage routings also what the second per-lane kernel re-runs:
+ * config 5's P = 3 instances, or config 4's instances that outgrew the tight
+ * layout), out2[1] = by a second per-lane kernel (two-stage routings only).
+ * What reaches the general kernel is out2[1] for two-stage chunks, out2[0]
+ * otherwise.  A list that overflowed counts cap + 1 more.  Waits for the
+ * device; reset != 0 zeroes the counts after reading.  Observability only:
+ * results never depend on it.                                                */
+int pxb_handoff_counts(int dev, uint64_t* out2, int reset);
 
 /* ---- misc ----------------------------------------------------------------- */
 const char* pxb_strerror(int code);

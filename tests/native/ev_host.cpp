@@ -54,13 +54,16 @@ struct HostMem {
     PXB_HCHK(i < n && half < 2u);
     reinterpret_cast<uint16_t*>(w + i)[half] = (uint16_t)v;
   }
+  // (the device's lane-interleaved halfword arrays: per lane, halfword i of the array at word base)
+  uint32_t ldh(uint32_t base, uint32_t i) const { return ld16(base, i); }
+  void sth(uint32_t base, uint32_t i, uint32_t v) const { st16(base, i, v); }
   void orw(uint32_t i, uint32_t v) const { PXB_HCHK(i < n); w[i] |= v; }
 };
 
-template <int PM, int N, int W, bool CMP, bool LG, bool SL, bool SP>
+template <int PM, int N, int W, bool CMP, bool LG, bool SL, int SP>
 int run_shape(const pxb_config* cfg, pxb_result* out, uint32_t* dig, pxb_acceptor_rec* acc, int64_t* tot,
               uint32_t* bail_ids, uint32_t* n_bail, uint64_t* micro_steps) {
-  constexpr int POOL = EvPool<PM, N, CMP, LG, SL>::value;
+  constexpr int POOL = EvPool<PM, N, CMP, LG, SL, SP>::value;
   using S = Shape<PM, N, POOL, W, CMP, LG, SL, SP>;
   g_words = S::WORDS;
   // garbage: init must set what it reads (checked builds: exactly WORDS, so
@@ -133,7 +136,7 @@ int run_shape(const pxb_config* cfg, pxb_result* out, uint32_t* dig, pxb_accepto
   return 0;
 }
 
-template <int PM, int W, bool CMP, bool LG, bool SL, bool SP>
+template <int PM, int W, bool CMP, bool LG, bool SL, int SP>
 int run_n(const pxb_config* c, pxb_result* o, uint32_t* d, pxb_acceptor_rec* a, int64_t* t, uint32_t* b, uint32_t* nb,
           uint64_t* ms) {
   switch (c->n_acceptors) {
@@ -151,7 +154,7 @@ int run_n(const pxb_config* c, pxb_result* o, uint32_t* d, pxb_acceptor_rec* a, 
   return -1;
 }
 
-template <int W, bool CMP, bool LG = false, bool SL = false, bool SP = false>
+template <int W, bool CMP, bool LG = false, bool SL = false, int SP = 0>
 int run_w(const pxb_config* c, uint32_t pm, pxb_result* o, uint32_t* d, pxb_acceptor_rec* a, int64_t* t, uint32_t* b,
           uint32_t* nb, uint64_t* ms) {
   switch (pm) {
@@ -170,8 +173,8 @@ extern "C" int ev_host_run(const pxb_config* cfg, pxb_result* out, uint32_t* dig
   const char* lv = getenv("EV_LAYOUT");                 // tests: force a layout
   const int layout = lv ? atoi(lv) : layout_for(cfg);
   if (layout == 2 && cfg->delay_max > 8) return -1;
-  if ((layout == 3 || layout == 6) && cfg->delay_max > 4) return -1;
-  if (layout == 6 && (cfg->loss_ppm || cfg->skew_max || (cfg->flags & PXB_CFG_RANDOMIZE) || cfg->n_ticks > 1)) return -1;
+  if ((layout == 3 || layout == 6 || layout == 7) && cfg->delay_max > 4) return -1;
+  if ((layout == 6 || layout == 7) && (cfg->loss_ppm || cfg->skew_max || (cfg->flags & PXB_CFG_RANDOMIZE) || cfg->n_ticks > 1)) return -1;
   if ((layout == 4) != (cfg->n_ticks > 1)) return -1;      // log mode runs on the log-mode fields only
   if ((layout == 0 || layout == 5) && cfg->delay_max > 8) return -1;
   // tests: the shape's proposer capacity; below n_proposers (fuzzed batches
@@ -190,7 +193,8 @@ extern "C" int ev_host_run(const pxb_config* cfg, pxb_result* out, uint32_t* dig
     case 3: return run_w<4, true>(cfg, pm, out, dig, acc, totals, bail_ids, n_bail, micro_steps);
     case 4: return run_w<8, false, true>(cfg, pm, out, dig, acc, totals, bail_ids, n_bail, micro_steps);
     case 5: return run_w<8, false, false, true>(cfg, pm, out, dig, acc, totals, bail_ids, n_bail, micro_steps);
-    case 6: return run_w<4, true, false, false, true>(cfg, pm, out, dig, acc, totals, bail_ids, n_bail, micro_steps);
+    case 6: return run_w<4, true, false, false, 1>(cfg, pm, out, dig, acc, totals, bail_ids, n_bail, micro_steps);
+    case 7: return run_w<4, true, false, false, 2>(cfg, pm, out, dig, acc, totals, bail_ids, n_bail, micro_steps);
   }
   return -1;
 }

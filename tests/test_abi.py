@@ -23,7 +23,7 @@ def test_header_declares_the_boundary():
     names = _declared()
     for f in ("pxb_run", "pxb_run_device", "pxb_acceptor_handle", "pxb_proposer_handle",
               "pxb_strerror", "pxb_last_hip_error", "pxb_abi_version", "pxb_init", "pxb_shutdown",
-              "pxb_run_multi"):
+              "pxb_run_multi", "pxb_stream_release", "pxb_handoff_counts"):
         assert f in names
 
 
@@ -60,7 +60,13 @@ int main(void) {
 
 def test_misc_entry_points_without_gpu():
     lib = pxb.load()
-    assert lib.pxb_abi_version() == 3
+    assert lib.pxb_abi_version() == 4            # 4: pxb_stream_release, pxb_handoff_counts
+    assert "#define PXB_ABI_VERSION 4" in open(HEADER).read()
+    # no scratch on a device yet (no GPU here): zero counts, no HIP call
+    out = (C.c_uint64 * 2)(7, 7)
+    assert lib.pxb_handoff_counts(0, C.cast(out, C.c_void_p), 0) == 0 and list(out) == [0, 0]
+    assert lib.pxb_handoff_counts(0, None, 0) == pxb.PXB_E_INVAL
+    assert lib.pxb_handoff_counts(64, C.cast(out, C.c_void_p), 0) == pxb.PXB_E_INVAL
     assert lib.pxb_strerror(pxb.PXB_E_INVAL) == b"invalid argument"
     assert lib.pxb_canonical_bytes_nofault(5) == 1140
 

@@ -292,6 +292,83 @@ def test_config5_split_matches_other_routings(gpu_lib, first):
         assert a[3] == b[3], env
 
 
+def _with_env(env, fn):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return fn()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("first", [31337, (1 << 32) - 25000])
+def test_config4_tight_matches_other_routings(gpu_lib, first):
+    """Config 4 runs tight: layout 7 (52 LDS words, 12 waves per CU) over the
+    chunk, layout 6 over the instances it handed on, the general kernel over
+    that one's.  Identical to layout 6 alone (PXB_NO_TIGHT=1) and to the
+    general kernel alone (PXB_NO_EV=1); the tight launch does hand some on."""
+    cfg = pxb.CONFIGS[4]
+    pxb.handoff_counts(0, reset=True)
+    a = pxb.run(cfg, first, 60000, want_acceptors=True)
+    h1, h2 = pxb.handoff_counts(0, reset=True)
+    assert h1 > 0 and h2 <= h1
+    for env in ("PXB_NO_TIGHT", "PXB_NO_EV"):
+        b = _with_env({env: "1"}, lambda: pxb.run(cfg, first, 60000, want_acceptors=True))
+        for x, y in zip(a[:3], b[:3]):
+            assert np.array_equal(x, y), env
+        assert a[3] == b[3], env
+
+
+@pytest.mark.parametrize("cap", [0, 40, 1 << 20])
+def test_config4_tight_list_overflow(gpu_lib, cap):
+    """The tight routing's id lists capped (0: the layout-7 list overflows at
+    once, so layout 6 runs nothing and the general kernel re-runs the chunk;
+    40: either list may overflow): exact either way."""
+    _with_env({"PXB_EV_BAIL_CAP": str(cap)}, lambda: _cmp(pxb.CONFIGS[4], (1 << 31) + 5, 30000))
+
+
+def test_config4_contiguous_at_production_bail_rate(gpu_lib):
+    """2^21 contiguous config-4 instances, bit-exact against the oracle
+    (results, digests, totals) through both routings: the tight one (layout 7
+    hands ~0.5 % on to layout 6, which hands a few on to the general kernel)
+    and layout 6 alone (~0.01 % to the general kernel).  Each hand-off path
+    carries at least 100 instances, so the hand-offs are exercised at the
+    north star's own rate, not only at small sizes."""
+    cfg, first, n = pxb.CONFIGS[4], 1 << 36, 1 << 21
+    eres, edig, _, ecnt = oracle_c.run_cpu(cfg, first, n, threads=THREADS)
+    for env in ({}, {"PXB_NO_TIGHT": "1"}):
+        pxb.handoff_counts(0, reset=True)
+        res, dig, _, cnt = _with_env(env, lambda: pxb.run(cfg, first, n))
+        h1, h2 = pxb.handoff_counts(0, reset=True)
+        bad = np.nonzero((res != eres).any(axis=1))[0]
+        assert bad.size == 0, "%s: first mismatch at %d" % (env, first + bad[0])
+        assert np.array_equal(dig, edig) and cnt == ecnt, env
+        if env:
+            assert h1 >= 100 and h2 == 0, (env, h1, h2)          # layout 6 -> general kernel
+        else:
+            assert h1 >= 5000 and h2 >= 1, (h1, h2)              # layout 7 -> layout 6 -> general
+
+
+def test_config5_contiguous_at_production_bail_rate(gpu_lib):
+    """2^20 contiguous config-5 instances (the split routing: the two-proposer
+    shape over the chunk, the three-proposer shape over the P = 3 third, the
+    general kernel over its bails), bit-exact against the oracle, with >= 100
+    instances reaching the general kernel."""
+    cfg, first, n = pxb.CONFIGS[5], 3 << 34, 1 << 20
+    eres, edig, _, ecnt = oracle_c.run_cpu(cfg, first, n, threads=THREADS)
+    pxb.handoff_counts(0, reset=True)
+    res, dig, _, cnt = pxb.run(cfg, first, n)
+    h1, h2 = pxb.handoff_counts(0, reset=True)
+    bad = np.nonzero((res != eres).any(axis=1))[0]
+    assert bad.size == 0, "first mismatch at %d" % (first + bad[0])
+    assert np.array_equal(dig, edig) and cnt == ecnt
+    assert h1 > n // 4 and h2 >= 100, (h1, h2)
+
+
 @pytest.mark.parametrize("cap", [0, 5000])
 def test_config5_split_list_overflow(gpu_lib, cap):
     """The split routing's id lists overflowing (cap 0: the P = 3 list, so the

@@ -1,5 +1,5 @@
 """A/B timing of per-lane-kernel library variants (diagnostic; never the bench
-number).  python tools/ab_ev.py lib1.so [lib2.so ...]
+number).  python tools/ab_ev.py lib1.so[@PXB_X=1] [lib2.so ...]
 Per lib: configs 4 (2^23), 3 (2^22), 5 (2^22): kernel ms per launch (HIP
 events on the launch stream) and the run totals, which must equal the first
 lib's (every variant is exact)."""
@@ -37,7 +37,14 @@ def timeit(cfg, n, reps):
 
 def main():
     ref = {}
-    for lib in sys.argv[1:]:
+    for arg in sys.argv[1:]:
+        # lib.so[@VAR=value,VAR=value]: the variant's environment (routing switches)
+        lib, _, envs = arg.partition("@")
+        for k in [k for k in os.environ if k.startswith("PXB_")]:
+            del os.environ[k]
+        for kv in filter(None, envs.split(",")):
+            k, _, v = kv.partition("=")
+            os.environ[k] = v
         pxb._lib = None
         pxb.load(os.path.join(ROOT, lib))
         row = []
@@ -45,7 +52,7 @@ def main():
             ms, t = timeit(pxb.CONFIGS[c], n, reps)
             ok = ref.setdefault((c, n), t) == t
             row.append("c%d %8.2f ms %6.1f M/s%s" % (c, ms, n / ms / 1e3, "" if ok else " TOTALS DIFFER"))
-        print("%-26s %s" % (os.path.basename(lib), " | ".join(row)), flush=True)
+        print("%-26s %s" % (os.path.basename(lib) + ("@" + envs if envs else ""), " | ".join(row)), flush=True)
 
 
 if __name__ == "__main__":

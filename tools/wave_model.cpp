@@ -35,15 +35,17 @@ struct HostMem {
   void st16(uint32_t base, uint32_t i, uint32_t v) const { reinterpret_cast<uint16_t*>(w + base)[i] = (uint16_t)v; }
   uint32_t ld16h(uint32_t i, uint32_t half) const { return reinterpret_cast<const uint16_t*>(w + i)[half]; }
   void st16h(uint32_t i, uint32_t half, uint32_t v) const { reinterpret_cast<uint16_t*>(w + i)[half] = (uint16_t)v; }
+  uint32_t ldh(uint32_t base, uint32_t i) const { return ld16(base, i); }
+  void sth(uint32_t base, uint32_t i, uint32_t v) const { st16(base, i, v); }
   void orw(uint32_t i, uint32_t v) const { w[i] |= v; }
 };
 
 constexpr int NB = 10;
 const char* names[NB] = {"END", "FIN", "RUN", "TICK_ENTER", "TICK_END", "ACC", "PROP", "COPY", "SEND1", "BCAST"};
 
-template <int PM, int N, int W, bool CMP, bool LG, bool SL, bool SP = false>
+template <int PM, int N, int W, bool CMP, bool LG, bool SL, int SP = 0>
 void model(const pxb_config* cfg, uint32_t n, uint32_t refill_min) {
-  constexpr int POOL = EvPool<PM, N, CMP, LG, SL>::value;
+  constexpr int POOL = EvPool<PM, N, CMP, LG, SL, SP>::value;
   using S = Shape<PM, N, POOL, W, CMP, LG, SL, SP>;
   const EvParams p = make_params(cfg);
   using Lane = EvLane<PM, N, POOL, W, CMP, HostMem, true, LG, SL, SP>;
@@ -141,7 +143,8 @@ int main(int argc, char** argv) {
   } else if (c == 4) {
     cfg.seed = 0x5EED0004; cfg.n_proposers = 2; cfg.n_acceptors = 7; cfg.delay_max = 4;
     cfg.crash_ppm = 200000; cfg.crash_len_max = 16; cfg.crash_start_max = 8; cfg.step_cap = 256;
-    model<2, 7, 4, true, false, false, true>(&cfg, n, rmin);   // layout 6 (simple schedule)
+    if (getenv("TIGHT")) model<2, 7, 4, true, false, false, 2>(&cfg, n, rmin);   // layout 7 (tight)
+    else model<2, 7, 4, true, false, false, 1>(&cfg, n, rmin);   // layout 6 (simple schedule)
   } else {
     fprintf(stderr, "config 3 or 4\n");
     return 1;
