@@ -286,15 +286,19 @@ constexpr uint32_t EV_BAIL_CAP = 1u << 22;
 constexpr uint64_t EV_SPLIT_CHUNK = 1ull << 25;
 constexpr uint32_t EV_SPLIT_CAP = (uint32_t)(EV_SPLIT_CHUNK / 2);
 // At most EV_LIST_STREAMS streams per device hold lists (created lazily, 16 MB
-// each + 64 MB for split routing).  An entry records an event behind the last
-// launches that use its lists; they are enqueued with g_mu held, so whoever
-// takes the entry over later (a stream beyond EV_LIST_STREAMS evicting the
-// oldest, or a new stream taking one that pxb_stream_release freed) first
-// waits for that event: two streams never share a list while either may
-// still run on it.
+// each + 64 MB for the two-stage routings).  An entry records an event behind
+// the last launches that use its lists (on every exit of a chunk once one of
+// them is queued, failures included); they are enqueued with g_mu held, so
+// whoever takes the entry over later (a stream beyond EV_LIST_STREAMS evicting
+// the oldest, or any stream taking one that pxb_stream_release freed) first
+// makes its own stream wait for that event (hipStreamWaitEvent: no host wait,
+// so no thread blocks under g_mu): two streams never share a list while
+// either may still run on it.  Ownership is a flag, not the stream handle:
+// the null (default) stream is a stream like any other.
 constexpr int EV_LIST_STREAMS = 8;
 struct EvLists {
-  hipStream_t s;                // owner (nullptr: free, buffers kept for the next owner)
+  hipStream_t s;                // owner, when owned
+  bool owned;                   // (false: free, buffers kept for the next owner)
   uint32_t* bail;
   uint32_t* split;
   hipEvent_t ev;                // behind the owner's last launches on these lists
@@ -364,21 +368,23 @@ int pxb_debug_wave_times(unsigned long long* out, unsigned max_waves) {
 int pxb_last_hip_error(void) { return g_last_hip; }
 
 // the bailed-id lists of (dev, stream) (callers hold g_mu until their launches
-// on the lists are enqueued and list_used() has recorded the entry's event)
+// on the lists are enqueued and a ListUse has recorded the entry's event)
 static int stream_lists(int dev, hipStream_t st, bool need_split, uint32_t** bail, uint32_t** split,
                         EvLists** ent) {
   EvLists* e = nullptr;
   for (int k = 0; k < g_nlists[dev] && !e; ++k)
-    if (g_lists[dev][k].s == st) e = &g_lists[dev][k];
+    if (g_lists[dev][k].owned && g_lists[dev][k].s == st) e = &g_lists[dev][k];
+  bool handover = e == nullptr;
   for (int k = 0; k < g_nlists[dev] && !e; ++k)      // a freed entry (its owner released it)
-    if (g_lists[dev][k].s == nullptr) e = &g_lists[dev][k];
+    if (!g_lists[dev][k].owned) e = &g_lists[dev][k];
   if (!e) {
     if (g_nlists[dev] < EV_LIST_STREAMS) e = &g_lists[dev][g_nlists[dev]++];
     else e = &g_lists[dev][g_lnext[dev]++ % EV_LIST_STREAMS];   // every entry owned: take the oldest over
   }
-  if (e->s != st) {                                  // new owner: the old one's launches must be done
-    if (e->ev_set) HIPCHK(hipEventSynchronize(e->ev));
+  if (handover) {                                    // new owner: after the old owner's launches
+    if (e->ev_set) HIPCHK(hipStreamWaitEvent(st, e->ev, 0));
     e->s = st;
+    e->owned = true;
   }
   if (!e->ev) HIPCHK(hipEventCreateWithFlags(&e->ev, hipEventDisableTiming));
   if (!e->bail) HIPCHK(hipMalloc(&e->bail, (size_t)EV_BAIL_CAP * sizeof(uint32_t)));
@@ -389,22 +395,27 @@ static int stream_lists(int dev, hipStream_t st, bool need_split, uint32_t** bai
   return PXB_OK;
 }
 
-// after the launches that use an entry's lists are enqueued on its stream (g_mu held)
-static int list_used(EvLists* e, hipStream_t st) {
-  HIPCHK(hipEventRecord(e->ev, st));
-  e->ev_set = true;
-  return PXB_OK;
-}
+// Records an entry's event behind the launches of a chunk that use its lists,
+// on every exit of the chunk (success or failure) once the first of them is
+// queued (g_mu held: declared after the chunk's lock, so destroyed before it)
+struct ListUse {
+  EvLists* e;
+  hipStream_t st;
+  bool queued = false;
+  ~ListUse() {
+    if (e && queued && hipEventRecord(e->ev, st) == hipSuccess) e->ev_set = true;
+  }
+};
 
 // A stream that is about to be destroyed gives up its lists (paxos_multi.cpp
 // creates a stream per device and call): the entry is freed for the next stream
 // (which waits for the event first), so lists never outlive their stream's use.
 extern "C" void pxb_stream_release(int dev, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  if (dev < 0 || dev >= 64 || !st) return;
+  if (dev < 0 || dev >= 64) return;
   std::lock_guard<std::mutex> lk(g_mu);
   for (int k = 0; k < g_nlists[dev]; ++k)
-    if (g_lists[dev][k].s == st) g_lists[dev][k].s = nullptr;
+    if (g_lists[dev][k].owned && g_lists[dev][k].s == st) g_lists[dev][k].owned = false;
 }
 
 // per-device scratch of pxb_run_device (callers hold g_mu)
@@ -556,6 +567,10 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
   // it runs first, over the chunk, and lists the instances that drew P = 3
   // (bailed at init) for the three-proposer shape, whose own bails go to the
   // general kernel.  PXB_NO_SPLIT=1 turns it off.
+  // tests only: PXB_FAIL_AFTER_FIRST=1 fails every chunk right after its first
+  // per-lane launch (the list and slot bookkeeping of the failure path)
+  const char* faf = getenv("PXB_FAIL_AFTER_FIRST");
+  const bool fail_after_first = faf && atoi(faf) > 0;
   const char* no_split = getenv("PXB_NO_SPLIT");
   const bool may_split = use_ev && (cfg->flags & PXB_CFG_RANDOMIZE) && cfg->n_proposers == 3 &&
                          !(no_split && atoi(no_split) > 0);
@@ -706,6 +721,8 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
       if (use_ev || use_ff1 || use_ffp)
         if (int rc2 = stream_lists(dev, st, split, &bail, &slist, &lent)) return rc2;
     }
+    // the lists' event goes behind whatever this chunk queues, on every exit
+    ListUse use{lent, st, lent != nullptr};
     // a launch that fails after an earlier one of this chunk has queued leaves
     // the slot half used: zero it behind the queued work before reporting
     auto fail = [&](hipError_t e) {
@@ -735,7 +752,7 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
       const uint64_t fres = (uint64_t)eocc * (uint64_t)cus;
       const unsigned fgrid = (unsigned)std::min<uint64_t>((nc + 255) / 256, fres);
       hipLaunchKernelGGL(ffn, dim3(fgrid), dim3(256), 0, st, fp);
-      HIPCHK(hipGetLastError());
+      if (hipError_t e = hipGetLastError()) return fail(e);
       kp.ids = bail;
       kp.n_ids = kp.queue + Q_BAIL;
       kp.ids_cap = bail_cap;
@@ -767,7 +784,7 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
       const uint64_t fres = (uint64_t)eocc * (uint64_t)cus;
       const unsigned fgrid = (unsigned)std::min<uint64_t>((nc + 255) / 256, fres);
       hipLaunchKernelGGL(pfn, dim3(fgrid), dim3(256), 0, st, fp);
-      HIPCHK(hipGetLastError());
+      if (hipError_t e = hipGetLastError()) return fail(e);
       kp.ids = bail;
       kp.n_ids = kp.queue + Q_BAIL;
       kp.ids_cap = bail_cap;
@@ -803,7 +820,9 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
         g_wt_waves = sgrid;
 #endif
         hipLaunchKernelGGL(sfn, dim3(sgrid), dim3(64), 0, st, sk);
-        HIPCHK(hipGetLastError());
+        if (hipError_t e = hipGetLastError()) return fail(e);
+        // (tests: a launch failure right after the first per-lane launch)
+        if (fail_after_first) return fail(hipErrorLaunchFailure);
         ek.ids = slist;
         ek.n_ids = kp.queue + Q_BAIL;
         ek.ids_cap = sk.bail_cap;
@@ -820,6 +839,7 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
 #endif
       hipLaunchKernelGGL(efn, dim3(egrid), dim3(64), 0, st, ek);
       if (hipError_t e = hipGetLastError()) return fail(e);
+      if (fail_after_first) return fail(hipErrorLaunchFailure);
       kp.ids = bail;
       kp.n_ids = kp.queue + bail_word;
       kp.ids_cap = bail_cap;
@@ -841,8 +861,6 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
     hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(TCOPIES), 0, st, kp.part, kp.part + ROWS_U64, kp.queue,
                        bail_word, bail_cap, totals, g_slots[dev] + HAND_U64);
     if (hipError_t e = hipGetLastError()) return fail(e);
-    if (lent)
-      if (int rc2 = list_used(lent, st)) return rc2;
   }
   return PXB_OK;
 }

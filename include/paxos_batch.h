@@ -151,10 +151,12 @@ int pxb_run(const pxb_config* cfg, pxb_result* out, uint32_t* log_digest,
  *     kernel for those, then the general faulty kernel over its bails;
  *   faulty single decree: the per-lane event kernel, then the general faulty
  *     kernel over its bailed instances; loss-free, skew-free batches with
- *     delays <= 4 (BASELINE config 4) take its simple-schedule shape; fuzzed
- *     three-proposer batches run the two-proposer event kernel first and the
- *     three-proposer one over the instances that drew P = 3 (chunks of 2^26;
- *     2^25 split);
+ *     delays <= 4 (BASELINE config 4) take its simple-schedule shape, and
+ *     with two proposers over more than 10 links its tight layout first
+ *     (12 waves per CU), the simple-schedule shape over what that hands on;
+ *     fuzzed three-proposer batches run the two-proposer event kernel first
+ *     and the three-proposer one over the instances that drew P = 3 (chunks
+ *     of 2^26; 2^25 split);
  *   faulty log mode (n_ticks > 1, delays <= 8): the per-lane event kernel's
  *     log-mode shape, then the general log-mode kernel over its bailed
  *     instances (chunks of 2^26; longer delays: the general log-mode kernel).
@@ -180,10 +182,11 @@ int pxb_run_multi(const pxb_config* cfg, int n_devices, pxb_result* out, uint32_
  * communicators of pxb_run_multi, created lazily on first use.  The per-lane
  * kernels' bailed-id lists are kept per (device, stream) of pxb_run_device,
  * allocated on that stream's first faulty or per-lane launch: 16 MB each, plus
- * 64 MB for the split routing of fuzzed three-proposer batches, for at most 8
- * streams per device (a ninth stream takes over the oldest entry once that
- * entry's last launches have completed: an event recorded behind them; a
- * stream destroyed by the library hands its entry back).  pxb_init(n) creates the launch slots of devices 0..n-1
+ * 64 MB for the two-stage routings (config 5's split, config 4's tight), for
+ * at most 8 streams per device (a ninth stream takes over the oldest entry:
+ * its launches wait on the device for an event recorded behind that entry's
+ * last launches, failed chunks included; a stream destroyed by the library
+ * hands its entry back).  pxb_init(n) creates the launch slots of devices 0..n-1
  * (n <= 0: all visible) up front; pxb_shutdown() waits for those devices, frees everything
  * and destroys the communicators; the next call starts afresh.  Both are
  * optional.  Do not call pxb_shutdown while other threads have calls in
@@ -194,11 +197,13 @@ int pxb_init(int n_devices);
 int pxb_shutdown(void);
 
 /* pxb_stream_release (ABI 4): `stream` (a hipStream_t used with pxb_run_device on device
- * `dev`) is about to be destroyed: its bailed-id lists go back to the library
- * for the next stream, which first waits for the event behind their last
- * launches.  Optional (without it a ninth stream takes the oldest entry over);
- * pxb_run_multi calls it for the streams it creates.  Unknown streams are
- * ignored.  First use of a stream allocates its lists: a timed loop should
+ * `dev`; NULL = the default stream) is about to be destroyed or has no more
+ * work for the library: its bailed-id lists go back to the library for the
+ * next stream, whose launches first wait (on the device, hipStreamWaitEvent)
+ * for the event behind their last launches, even while those still run.
+ * Optional (without it a ninth stream takes the oldest entry over the same
+ * way); pxb_run_multi calls it for the streams it creates.  Unknown streams
+ * are ignored.  First use of a stream allocates its lists: a timed loop should
  * make one small untimed launch on every stream it will use (bench.py does).  */
 void pxb_stream_release(int dev, void* stream);
 

@@ -633,6 +633,68 @@ def test_stream_release_with_caller_streams(gpu_lib):
         pxb.stream_release(0, 0)                  # (unknown / null streams are ignored)
 
 
+def _device_run(cfg, first, n, stream):
+    import torch
+    out = torch.zeros((n, 4), dtype=torch.int32, device="cuda")
+    dig = torch.zeros((n, cfg.n_acceptors), dtype=torch.int32, device="cuda")
+    tot = torch.zeros(16, dtype=torch.int64, device="cuda")
+    torch.cuda.current_stream().synchronize()     # (the zeros before the launch on `stream`)
+    pxb.run_device(cfg, first, n, d_results=out, d_digests=dig, d_totals=tot,
+                   stream=stream.cuda_stream if stream is not None else None)
+    return out, dig, tot
+
+
+def _host(out, dig, tot):
+    return (out.cpu().numpy().view(np.uint32), dig.cpu().numpy().view(np.uint32),
+            pxb.counters_dict(tot.cpu().tolist()))
+
+
+@pytest.mark.parametrize("c", [4, 5])
+def test_failure_after_first_launch_then_more_streams(gpu_lib, c):
+    """A chunk that fails right after its first per-lane launch (test hook
+    PXB_FAIL_AFTER_FIRST: the two-stage routings' first list is then in use by
+    a queued kernel) still records its lists' event, so the streams that take
+    those lists over later -- nine more streams, one past the device's eight
+    entries, then the failed stream again -- wait for that kernel: every run
+    after the failure is exact."""
+    import torch
+    cfg, n = pxb.CONFIGS[c], 30000
+    want = pxb.run(cfg, 4096, n)
+    bad = torch.cuda.Stream()
+    with pytest.raises(pxb.PaxosError):
+        _with_env({"PXB_FAIL_AFTER_FIRST": "1"}, lambda: _device_run(cfg, 4096, n, bad))
+    for st in [torch.cuda.Stream() for _ in range(9)] + [bad]:
+        res = _device_run(cfg, 4096, n, st)
+        st.synchronize()
+        got = _host(*res)
+        assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1]) and got[2] == want[3]
+
+
+def test_release_in_flight_then_default_stream(gpu_lib):
+    """A caller stream released while its launch still runs (its lists are
+    free for the next owner), then batches on the default stream, which takes
+    the entry over: the default stream waits for the released stream's event
+    on the device (ownership is a flag, so the null stream is an owner like
+    any other), and both streams' results are exact."""
+    import torch
+    cfg, n = pxb.CONFIGS[4], 1 << 20
+    want = pxb.run(cfg, 1 << 33, n)
+    small = pxb.run(cfg, 99, 20000)
+    st = torch.cuda.Stream()
+    dev = torch.cuda.current_device()
+    res = _device_run(cfg, 1 << 33, n, st)         # (~20 ms on the device)
+    pxb.stream_release(dev, st.cuda_stream)
+    for _ in range(3):
+        got = pxb.run(cfg, 99, 20000)               # (pxb_run: the default stream)
+        assert np.array_equal(got[0], small[0]) and got[3] == small[3]
+    st.synchronize()
+    got = _host(*res)
+    assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1]) and got[2] == want[3]
+    pxb.stream_release(dev, 0)                      # (the default stream's entry back too)
+    got = pxb.run(cfg, 99, 20000)
+    assert np.array_equal(got[0], small[0]) and got[3] == small[3]
+
+
 def test_config5_full_sweep_totals(gpu_lib):
     """BASELINE config 5 at its stated size: all 2^28 randomized schedules on
     one GPU in one call (run totals only, no per-instance outputs).  The
