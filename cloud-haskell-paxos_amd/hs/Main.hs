@@ -15,9 +15,12 @@ main = do
   let cfg = case args of
         ["stock"] -> defaultConfig { bcCount = 1 }   -- Main.hs:41,45: 2 servers, 2 clients
         _         -> config2
-  r <- runBatchMulti 0 cfg
-  case r of
-    Left err -> putStrLn ("pxb error: " ++ err)
-    Right (outs, tot) -> do
-      print tot
-      mapM_ print (take 4 outs)
+  -- the engine lives as long as this process (pxb_init at start, pxb_shutdown at exit)
+  e <- withEngine 0 $ do
+    r <- runBatchMulti 0 cfg
+    case r of
+      Left err -> putStrLn ("pxb error: " ++ err)
+      Right (outs, tot) -> do
+        print tot
+        mapM_ print (take 4 outs)
+  either (putStrLn . ("pxb init: " ++)) pure e

@@ -26,10 +26,17 @@ module PaxosBatch
   , runBatch
   , runBatchMulti
   , commandOf
+    -- * Lifecycle (the host owns it: app/Main.hs start and exit)
+  , abiVersion
+  , initDevices
+  , shutdown
+  , withEngine
+  , handoffCounts
   ) where
 
 import           Common                (Command, Proposal, Ticket (..))
 
+import           Control.Exception     (bracket_)
 import           Control.Monad         (forM)
 import           Data.Bits             (shiftR, testBit, (.&.))
 import           Data.Int              (Int32, Int64)
@@ -42,7 +49,7 @@ import           Foreign.Marshal.Utils (with)
 import           Foreign.Ptr           (Ptr, nullPtr)
 import           Foreign.Storable      (Storable (..))
 
--- | pxb_config (72 bytes, ABI 3, see include/paxos_batch.h).
+-- | pxb_config (72 bytes, unchanged since ABI 3, see include/paxos_batch.h).
 data BatchConfig = BatchConfig
   { bcSeed          :: !Word64
   , bcFirst         :: !Word64   -- ^ global id of the first instance
@@ -126,6 +133,66 @@ foreign import ccall safe "pxb_run_multi"
   c_pxb_run_multi :: Ptr BatchConfig -> CInt -> Ptr Word32 -> Ptr Word32 -> Ptr () -> Ptr Int64 -> IO CInt
 foreign import ccall unsafe "pxb_strerror"
   c_pxb_strerror :: CInt -> IO CString
+foreign import ccall unsafe "pxb_abi_version"
+  c_pxb_abi_version :: IO CInt
+foreign import ccall safe "pxb_init"
+  c_pxb_init :: CInt -> IO CInt
+foreign import ccall safe "pxb_shutdown"
+  c_pxb_shutdown :: IO CInt
+foreign import ccall safe "pxb_handoff_counts"
+  c_pxb_handoff_counts :: CInt -> Ptr Word64 -> CInt -> IO CInt
+
+-- | The ABI this module was written against (include/paxos_batch.h).
+expectedAbi :: Int
+expectedAbi = 4
+
+-- | pxb_abi_version of the loaded library.
+abiVersion :: IO Int
+abiVersion = fromIntegral <$> c_pxb_abi_version
+
+checked :: IO CInt -> IO (Either String ())
+checked act = do
+  rc <- act
+  if rc == 0 then pure (Right ()) else Left <$> (c_pxb_strerror rc >>= peekCString)
+
+-- | pxb_init: allocate the scratch of the first @g@ GPUs (all visible when
+-- @g <= 0@) up front, at process start (where app/Main.hs:27-36 brings the
+-- node up).  Optional: the first batch does it lazily.  Refuses a library
+-- built for another ABI.
+initDevices :: Int -> IO (Either String ())
+initDevices g = do
+  v <- abiVersion
+  if v /= expectedAbi
+    then pure (Left ("libpaxos_batch ABI " <> show v <> ", binding expects " <> show expectedAbi))
+    else checked (c_pxb_init (fromIntegral g))
+
+-- | pxb_shutdown: wait for the devices, free every scratch buffer and the
+-- cached RCCL communicators (process exit).  No batch may be running on
+-- another Haskell thread.
+shutdown :: IO (Either String ())
+shutdown = checked c_pxb_shutdown
+
+-- | Bracket a program's batches with 'initDevices' / 'shutdown', so the
+-- engine's lifetime is the host's, as the reference's node is
+-- (app/Main.hs:27-53).
+withEngine :: Int -> IO a -> IO (Either String a)
+withEngine g body = do
+  ok <- initDevices g
+  case ok of
+    Left err -> pure (Left err)
+    Right () -> Right <$> bracket_ (pure ()) (shutdown >>= either putStrLn pure) body
+
+-- | pxb_handoff_counts of GPU @dev@: instances the first per-lane kernel of a
+-- chunk handed on, and those a second one handed on (observability only).
+handoffCounts :: Int -> Bool -> IO (Either String (Word64, Word64))
+handoffCounts dev reset =
+  allocaArray 2 $ \p -> do
+    r <- checked (c_pxb_handoff_counts (fromIntegral dev) p (if reset then 1 else 0))
+    case r of
+      Left err -> pure (Left err)
+      Right () -> do
+        [a, b] <- peekArray 2 p
+        pure (Right (a, b))
 
 -- | Run a batch on the current GPU.
 runBatch :: BatchConfig -> IO (Either String ([Outcome], Totals))
