@@ -91,6 +91,7 @@ def check(exe, cfg, first, n, env=None, max_bail_frac=0.05):
 @pytest.mark.parametrize("layout,c,pm", [
     (None, 3, None),        # compact, 4-step wheel (layout 3)
     (None, 4, None),        # simple schedule (layout 6)
+    ("7", 4, None),         # tight simple schedule (layout 7: halfword response FIFOs with a sentinel)
     ("3", 4, None),         # config 4 on the general compact layout
     ("2", 3, None),         # compact, 8-step wheel
     ("0", 3, None),         # 4-entry FIFOs, 8-step wheel
