@@ -123,8 +123,10 @@ struct Shape {
   static constexpr int REQ = 0;                      // NLQ: request links, index a*PM + p (CMP: + reply seq)
   static constexpr int RSEQ = REQ + NLQ;             // !CMP: NLQ halfwords of reply seq, index a*PM + p
   // (slim: the reply seqs are bytes in registers)
-  static constexpr int RSP = RSEQ + ((CMP || SL) ? 0 : (NLQ + 1) / 2);   // NLQ response links, index p*N + a
-  static constexpr int POOLW = RSP + (RH ? (NLQ + 1) / 2 : NLQ);   // POOL response words (RH: links in halfwords)
+  static constexpr int RSP0 = RSEQ + ((CMP || SL) ? 0 : (NLQ + 1) / 2);   // NLQ response links, index p*N + a
+  // (RH: the halfword links go last, after the wheel, so that every pool
+  // load of a 5-bit entry, Round2Success codes included, stays in the lane's words)
+  static constexpr int POOLW = RH ? RSP0 : RSP0 + NLQ;   // POOL response words
   // broadcast ring slots per proposer: short-delay (compact) schedules never
   // hold more than 4 broadcasts of one proposer in flight (BASELINE configs
   // 3 and 4: the bail rate is the same with 4 slots as with 8), nor does
@@ -137,7 +139,8 @@ struct Shape {
   static constexpr int BRING = POOLZ + (LG ? POOL / 2 + 1 : 0);   // PM*BR payloads: halfwords (LG: words)
   static constexpr int CLOG = BRING + (LG ? PM * BR : PM * BR / 2);   // LG: PXB_LOG_TRACK halfwords
   static constexpr int WHEEL = CLOG + (LG ? PXB_LOG_TRACK / 2 : 0);   // W * WW due masks
-  static constexpr int WORDS = WHEEL + W * WW;
+  static constexpr int RSP = RH ? WHEEL + W * WW : RSP0;
+  static constexpr int WORDS = WHEEL + W * WW + (RH ? (NLQ + 1) / 2 : 0);
   static_assert(W == 4 || W == 8 || W == 16, "wheel of 4, 8 or 16 steps");
   static_assert(NIN <= 32 && NLQ <= 32, "masks are 32-bit");
   static_assert(RH ? (IB * RC <= 16 && CMP && W == 4) : RSN ? (IB * RC <= 32 && POOL < (1 << IB)) : (RD + 4 <= 32),
@@ -145,6 +148,8 @@ struct Shape {
   // (index + 1 below the Round2Success codes)
   static_assert(!(RZ && RCODE) || POOL < (int)RCB, "pool entries and codes");
   static_assert(!RH || (SP && !LG && RCODE && DB == 3), "layout 7: simple single decree, 4-step wheel");
+  // (every 5-bit entry indexes the lane's words: else send_first clamps the code's pool load)
+  static constexpr bool TE_SAFE = POOLW - POOLB_SHIFT + 31 < WORDS;
   static constexpr int POOLB = POOLW - POOLB_SHIFT;
   static_assert(QL + QLB <= 31, "request-link word");
 };
@@ -563,7 +568,7 @@ struct EvLane {
       accd[a] = 0x811C9DC5u;
     }
 #pragma unroll
-    for (int i = S::REQ; i < (S::RH ? S::RSP : S::POOLW); ++i) m.st(i, 0u);   // request links, reply seqs, response links
+    for (int i = S::REQ; i < S::POOLW; ++i) m.st(i, 0u);   // request links, reply seqs, response links (RH: below)
     if constexpr (S::RH) {                           // (halfword rows shared with the other lanes' words)
 #pragma unroll
       for (int i = 0; i < NLQ; ++i) m.sth(S::RSP, i, 1u);   // empty: the sentinel
@@ -696,7 +701,7 @@ struct EvLane {
       const uint32_t msb = 31u - (uint32_t)__builtin_clz(h | 1u);   // (h >= 1: the sentinel)
       const uint32_t te = (h >> ((msb - (uint32_t)S::IB) & 31u)) & IM;   // (empty: >> 27 = 0)
       // (a Round2Success code carries its due & 7; a code's or an empty link's pool load is unused)
-      const uint32_t tp = (m.ld(S::POOLB + te) >> 26) & 15u;
+      const uint32_t tp = (m.ld(S::POOLB + ((S::TE_SAFE || te < S::RCB) ? te : 0u)) >> 26) & 15u;
       const uint32_t rtail = (te >= S::RCB) ? te & 7u : tp;
       const uint32_t qlen = (wq >> S::QL) & QLM;
       const uint32_t qtail = (wq >> (((uint32_t)S::EB * qlen - (uint32_t)S::DB) & 31u)) & DM;

@@ -108,6 +108,16 @@ def test_baseline_layouts_sanitized(exe, layout, c, pm):
     check(exe, pxb.CONFIGS[c], 2024, 600, env, max_bail_frac=0.75 if pm == "2" else 0.05)
 
 
+@pytest.mark.parametrize("P,N", [(1, 2), (2, 5), (2, 9), (3, 9)])
+def test_tight_layout_topologies_sanitized(exe, P, N):
+    """Layout 7 on small and large topologies: its 5-bit response entries
+    (pool index + 1, or a Round2Success code) index only the lane's words (the
+    checked accessor asserts it; small shapes clamp a code's unused pool load)."""
+    cfg = pxb.Config(seed=0x7A + 16 * P + N, n_proposers=P, n_acceptors=N, delay_max=4, crash_ppm=250000,
+                     crash_len_max=12, crash_start_max=10, step_cap=300)
+    check(exe, cfg, 99, 300, {"EV_LAYOUT": "7"}, max_bail_frac=1.0)
+
+
 @pytest.mark.parametrize("P,N,delay", [(1, 9, 12), (3, 9, 15), (2, 5, 9)])
 def test_16step_wheel_sanitized(exe, P, N, delay):
     """Layout 1 (16-step wheel: delays above 8)."""
