@@ -59,6 +59,9 @@
 namespace pxb {
 namespace ev {
 
+#ifndef PXB_EV_STORE_BACK
+#define PXB_EV_STORE_BACK 1
+#endif
 #ifndef PXB_EV_PQ_CAP
 #define PXB_EV_PQ_CAP 4
 #endif
@@ -632,10 +635,19 @@ struct EvLane {
       if constexpr (LG) {
         m.st(S::BRING + q * S::BR + slot0, x0 | (z0 << 12) | (kind0 << 30));
         if (p1) m.st(S::BRING + q * S::BR + slot1, x1 | (ASK << 30));
-      } else {
+      } else if constexpr (!PXB_EV_STORE_BACK) {
         m.st16h(S::BRING + bring_word(q, slot0), bring_half(q, slot0), x0 | (z0 << 12) | (kind0 << 14));
         if (p1) m.st16h(S::BRING + bring_word(q, slot1), bring_half(q, slot1), x1 | (ASK << 14));
       }
+    }
+    if constexpr (!LG && PXB_EV_STORE_BACK) {
+      // (without a branch: a lane that makes no broadcast stores the slots'
+      // halfwords back; slot1 = slot0 + 1 mod BR, so the two never alias)
+      const uint32_t w0a = S::BRING + bring_word(q, slot0), h0a = bring_half(q, slot0);
+      const uint32_t w1a = S::BRING + bring_word(q, slot1), h1a = bring_half(q, slot1);
+      const uint32_t o0 = m.ld16h(w0a, h0a), o1 = m.ld16h(w1a, h1a);
+      m.st16h(w0a, h0a, p0 ? x0 | (z0 << 12) | (kind0 << 14) : o0);
+      m.st16h(w1a, h1a, p1 ? x1 | (ASK << 14) : o1);
     }
     pq |= (p0 ? ((q << 3) | slot0) << (5u * pq_len) : 0u) | (p1 ? ((q << 3) | slot1) << (5u * pq_len + 5u) : 0u);
     const uint32_t nb = (p0 ? 1u : 0u) + (p1 ? 1u : 0u);
