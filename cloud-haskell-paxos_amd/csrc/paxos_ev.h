@@ -59,6 +59,12 @@
 namespace pxb {
 namespace ev {
 
+#ifndef PXB_EV_SL_RH
+#define PXB_EV_SL_RH 1
+#endif
+#ifndef PXB_EV_LG_RH
+#define PXB_EV_LG_RH 0
+#endif
 #ifndef PXB_EV_STORE_BACK
 #define PXB_EV_STORE_BACK 1
 #endif
@@ -80,7 +86,10 @@ struct Shape {
   // response FIFOs in halfwords (3 entries of pool index + 1 or a Round2Success
   // code, zero above the length), so that a lane fits 52 LDS words (13 KB per
   // wave: 12 waves per CU, 3 on every SIMD); its bails re-run on layout 6
-  static constexpr bool RH = SP_ == 2;
+  // (also the faulty log-mode shape over <= 10 links on the 8-step wheel:
+  // 75 words with a 15-word pool, 8 waves per CU instead of 7)
+  static constexpr bool RH = SP_ == 2 || (PXB_EV_LG_RH && LG_ && PM_ * N_ <= 10 && W_ == 8) ||
+                             (PXB_EV_SL_RH && SL_ && PM_ == 2 && PM_ * N_ > 16 && PM_ * N_ <= 18 && W_ == 8);
   static constexpr bool CMP = CMP_;                  // compact links (see Layouts)
   static constexpr bool LG = LG_;                    // log mode (several Ticks, long logs; see Layouts)
   static constexpr bool SL = SL_;                    // slim 4-entry layout (see Layouts)
@@ -146,11 +155,11 @@ struct Shape {
   static constexpr int WORDS = WHEEL + W * WW + (RH ? (NLQ + 1) / 2 : 0);
   static_assert(W == 4 || W == 8 || W == 16, "wheel of 4, 8 or 16 steps");
   static_assert(NIN <= 32 && NLQ <= 32, "masks are 32-bit");
-  static_assert(RH ? (IB * RC <= 16 && CMP && W == 4) : RSN ? (IB * RC <= 32 && POOL < (1 << IB)) : (RD + 4 <= 32),
+  static_assert(RH ? (IB * RC <= 16 && POOL < (1 << IB) - 1) : RSN ? (IB * RC <= 32 && POOL < (1 << IB)) : (RD + 4 <= 32),
                 "response-link word");
   // (index + 1 below the Round2Success codes)
   static_assert(!(RZ && RCODE) || POOL < (int)RCB, "pool entries and codes");
-  static_assert(!RH || (SP && !LG && RCODE && DB == 3), "layout 7: simple single decree, 4-step wheel");
+  static_assert(!RH || (SP && !LG && RCODE && DB == 3) || ((LG || SL) && !RCODE), "halfword links: layouts 7, 4, 5");
   // (every 5-bit entry indexes the lane's words: else send_first clamps the code's pool load)
   static constexpr bool TE_SAFE = POOLW - POOLB_SHIFT + 31 < WORDS;
   static constexpr int POOLB = POOLW - POOLB_SHIFT;
@@ -713,17 +722,22 @@ struct EvLane {
       const uint32_t msb = 31u - (uint32_t)__builtin_clz(h | 1u);   // (h >= 1: the sentinel)
       const uint32_t te = (h >> ((msb - (uint32_t)S::IB) & 31u)) & IM;   // (empty: >> 27 = 0)
       // (a Round2Success code carries its due & 7; a code's or an empty link's pool load is unused)
-      const uint32_t tp = (m.ld(S::POOLB + ((S::TE_SAFE || te < S::RCB) ? te : 0u)) >> 26) & 15u;
-      const uint32_t rtail = (te >= S::RCB) ? te & 7u : tp;
+      const bool tcode = S::RCODE && te >= S::RCB;       // (without codes every entry is a pool word's)
+      const uint32_t tp = (m.ld(S::POOLB + ((S::TE_SAFE || !tcode) ? te : 0u)) >> 26) & 15u;
+      const uint32_t rtail = tcode ? te & 7u : tp;
       const uint32_t qlen = (wq >> S::QL) & QLM;
       const uint32_t qtail = (wq >> (((uint32_t)S::EB * qlen - (uint32_t)S::DB) & 31u)) & DM;
       const uint32_t nz = isR ? h - 1u : qlen;           // (0: the link is empty)
-      const uint32_t rel = ((isR ? rtail : qtail) - b4) & (nz ? 7u : 0u);   // (DM = 7: the 4-step wheel)
+      // (a code's due is mod 8: RCODE only on the 4-step wheel, DM = 7; log
+      // mode's pool dues and request dues are mod 16)
+      constexpr uint32_t RM = S::RCODE ? 7u : 15u;
+      static_assert(!S::RCODE || DM == 7u, "codes on the 4-step wheel");
+      const uint32_t rel = ((isR ? rtail : qtail) - b4) & (nz ? (isR ? RM : DM) : 0u);
       due_rel = d > rel ? d : rel;
       due4 = (b4 + due_rel) & 15u;
       const bool rfull = h >= (1u << (S::IB * S::RC));
       // (as integers: a select of two booleans became five instructions)
-      const uint32_t pool_out = (pfree == 0) & !r2c ? 1u : 0u;
+      const uint32_t pool_out = ((pfree == 0) & !r2c) ? 1u : 0u;
       const uint32_t full = isR ? (h >> (S::IB * S::RC)) | pool_out : qlen >> 2;   // (QC = 4, qlen <= 4)
       static_assert(S::QC == 4, "request FIFOs of 4");
       bailed = bailed | (go & (full != 0u));
@@ -733,6 +747,10 @@ struct EvLane {
       // the pool word: to a free entry (harmless unless a reply goes), or, with
       // none free, to the request word, which the next store rewrites
       m.st(pfree ? S::POOLB + k2 : S::REQ + Lq, rp.pw | (due4 << 26));
+      if constexpr (LG) {                            // (entry k2 = pool index + 1; no free entry: the dummy halfword)
+        const uint32_t zi = pfree ? k2 - 1u : (uint32_t)POOL;
+        m.st16h(S::POOLZ + (zi >> 1), zi & 1u, rp.z);
+      }
       const uint32_t ent = r2c ? S::RCB + (due4 & 7u) : k2;
       // (the entry replaces the sentinel, the sentinel moves up one entry)
       const uint32_t nR = h + ((ent + (1u << S::IB) - 1u) << msb);
@@ -1012,7 +1030,8 @@ struct EvLane {
       const bool rkeep = resp & (S::RH ? rr >= (1u << (2 * S::IB)) : S::RZ ? nk != 0u : rlen > 1u) & nnow;
       in_mask = (pin & !rkeep) ? (in_mask & ~(1u << j)) : in_mask;
       const uint32_t rkind = pe >> 30, px = pe & 0xFFFu, py = (pe >> 12) & 0xFFFu;
-      const uint32_t pz = LG ? m.ld16h(S::POOLZ + (k >> 1), k & 1u) : (pe >> 24) & 3u;
+      const uint32_t kz = k - (uint32_t)S::POOLB_SHIFT;   // (the pool index of entry k)
+      const uint32_t pz = LG ? m.ld16h(S::POOLZ + ((kz >> 1) & 31u), kz & 1u) : (pe >> 24) & 3u;
       canon += resp ? 2u * (16u >> rkind) : 0u;         // Round1OK 16, HaveTicket 8, Round2Success 4
 
       const uint32_t w0 = get(pw0, q), w1 = get(pw1, q);

@@ -79,27 +79,36 @@ struct EvKParams {
 #endif
 // (log mode over at most 10 links: 18 words, which faulty log mode's batch never
 // fills (extra.log_mode_faulty: no bail in 20000 instances): 85 words per lane,
-// 7 waves per CU instead of 5)
+// 7 waves per CU instead of 5.  Round 5 measured the halfword response links
+// here too (PXB_EV_LG_RH=1 with PXB_EV_LG_POOL=15: 75 words, 8 waves per CU,
+// 9 bails in 20000): 2^22 +-1 %, 2^20 -11 % (the chunk tail): not used)
 // (slim: 44 words hold the responses of 99.6 % of config 5's P = 3 instances
 // (with its 5-deep response FIFOs, whose entries are pool index + 1: < 64
-// words), 30 those of 99.99 % of its P = 2 ones; compact over <= 10 links:
+// words), 28 those of 99.8 % of its P = 2 ones with halfword response links
+// (75 words per lane, 8 waves per CU; round 4: 30 words and 86, 7); compact over <= 10 links:
 // config 3 bails no more with 16 words than with 24, and its shape then leaves
 // LDS to spare at 12 waves per CU)
 // (tight, layout 7: 21 words, 50 per lane: 12 resident waves per CU need
 // <= 50 (measured: 52-word lanes ran 11, the 12th block waited); 5-bit
 // entries of pool index + 1 beside the 8 Round2Success codes allow <= 23;
 // config 4 bails 0.76 % on it, host model)
+#ifndef PXB_EV_SL2_POOL
+#define PXB_EV_SL2_POOL 28
+#endif
+#ifndef PXB_EV_LG_POOL
+#define PXB_EV_LG_POOL 18
+#endif
 #ifndef PXB_EV_TIGHT_POOL
 #define PXB_EV_TIGHT_POOL 21
 #endif
 template <int PM, int N, bool CMP, bool LG = false, bool SL = false, int SP = 0>
 struct EvPool {
   static constexpr int value = (SP == 2)             ? PXB_EV_TIGHT_POOL
-                               : (LG && PM * N <= 10)  ? 18
+                               : (LG && PM * N <= 10)  ? PXB_EV_LG_POOL
                                : (CMP && PM * N <= 10) ? 16
                                : (PM * N <= 16)      ? (CMP ? PXB_EV_CMP_POOL : 32)
                                : CMP                ? 48
-                               : (PM * N <= 18)     ? (SL ? 30 : 32)
+                               : (PM * N <= 18)     ? (SL ? PXB_EV_SL2_POOL : 32)
                                : SL                 ? 44
                                                     : 64;
 };

@@ -33,8 +33,10 @@ def lib():
     if _lib is None:
         if not os.path.exists(OUT) or any(os.path.getmtime(d) > os.path.getmtime(OUT) for d in DEPS):
             os.makedirs(os.path.dirname(OUT), exist_ok=True)
+            tmp = "%s.%d" % (OUT, os.getpid())          # (parallel workers: build, then rename)
             subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O2", "-std=c++17", "-fPIC", *DEFS,
-                            "-shared", "-o", OUT, SRC], check=True)
+                            "-shared", "-o", tmp, SRC], check=True)
+            os.replace(tmp, OUT)
         _lib = C.CDLL(OUT)
     return _lib
 
@@ -293,7 +295,7 @@ def test_random_log_mode_schedules(i):
     (-4, 2, 50, 12),     # tight (layout 7: halfword response FIFOs, 21-word pool)
     (3, 2, 44, 12),      # compact, 16-word pool (12 = the VGPR limit)
     (5, 3, 120, 5),      # slim, P = 3 share
-    (5, 2, 86, 7),       # slim, P <= 2 share
+    (5, 2, 75, 8),       # slim, P <= 2 share (halfword response links, 28-word pool)
     (7, 2, 85, 7),       # faulty log mode
 ])
 def test_layout_words_leave_lds_to_spare(c, pm, words, blocks, monkeypatch):

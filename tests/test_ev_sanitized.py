@@ -40,7 +40,11 @@ FLAGS = ["--offload-arch=gfx950", "-O1", "-g0", "-std=c++17", "-DPXB_HOST_CHECKE
 def exe():
     if not os.path.exists(EXE) or any(os.path.getmtime(d) > os.path.getmtime(EXE) for d in DEPS):
         os.makedirs(os.path.dirname(EXE), exist_ok=True)
-        subprocess.run(["/opt/rocm/bin/hipcc", *FLAGS, "-o", EXE, SRC], check=True, timeout=600)
+        # (built under a name of its own, then renamed: parallel test workers may
+        # build at once, and none may run a half-written binary)
+        tmp = "%s.%d" % (EXE, os.getpid())
+        subprocess.run(["/opt/rocm/bin/hipcc", *FLAGS, "-o", tmp, SRC], check=True, timeout=600)
+        os.replace(tmp, EXE)
     return EXE
 
 
