@@ -31,9 +31,14 @@ IGNORED = ("elementwise", "fill", "copy", "memset", "Memset", "Memcpy", "tile_su
 
 
 def _tag(name):
+    """The kernel's instantiation, e.g. 'paxos_ev_kernel<2, 7, 4, true, false, false, 2>'
+    (two-stage routings run two instantiations of one kernel template: each is
+    reported on its own, so the dominant one's average is a per-launch time)."""
     for t in KERNEL_TAGS:
         if t in name:
-            return t
+            i = name.index(t)
+            j = name.find("(", i)
+            return name[i:j] if j > i else name[i:]
     if name and not any(i in name for i in IGNORED):
         # an untagged kernel would silently drop out of the per-instance sums
         raise SystemExit("roofline.py: profiled kernel %r matches no KERNEL_TAGS entry" % name)
