@@ -284,6 +284,11 @@ constexpr uint32_t EV_BAIL_CAP = 1u << 22;
 // for the slots split launches use; config 5 at 2^25: 34.9 M/s with 2^24
 // chunks, 36.2 with 2^25)
 constexpr uint64_t EV_SPLIT_CHUNK = 1ull << 25;
+// fault-free per-lane kernels: blocks per launch, in multiples of the resident
+// ones (the dispatcher then hands a freed CU the next block, which balances
+// waves that run slower; one 2^28 config-2 launch: x1 5.26 ms, x2 4.76, x4 4.42,
+// x8 4.30, x16 4.25)
+constexpr uint64_t FF1_OVERSUB = 16;
 constexpr uint32_t EV_SPLIT_CAP = (uint32_t)(EV_SPLIT_CHUNK / 2);
 // At most EV_LIST_STREAMS streams per device hold lists (created lazily, 16 MB
 // each + 64 MB for the two-stage routings).  An entry records an event behind
@@ -749,7 +754,10 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
       fp.bail_cap = bail_cap;
       const char* fb = getenv("PXB_FF1_BAIL");           // tests: hand every instance to the general kernel
       fp.bail_all = (fb && atoi(fb) > 0) ? 1u : 0u;
-      const uint64_t fres = (uint64_t)eocc * (uint64_t)cus;
+      // FF1_OVERSUB x the resident blocks (PXB_FF1_OVERSUB=k: k, A/B)
+      const char* fos = getenv("PXB_FF1_OVERSUB");
+      const uint64_t over = (fos && atoi(fos) > 0 && atoi(fos) <= 64) ? (uint64_t)atoi(fos) : FF1_OVERSUB;
+      const uint64_t fres = (uint64_t)eocc * (uint64_t)cus * over;
       const unsigned fgrid = (unsigned)std::min<uint64_t>((nc + 255) / 256, fres);
       hipLaunchKernelGGL(ffn, dim3(fgrid), dim3(256), 0, st, fp);
       if (hipError_t e = hipGetLastError()) return fail(e);
@@ -781,7 +789,9 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
       fp.bail_cap = bail_cap;
       const char* fb = getenv("PXB_FF1_BAIL");           // tests: hand every instance to the general kernel
       fp.bail_all = (fb && atoi(fb) > 0) ? 1u : 0u;
-      const uint64_t fres = (uint64_t)eocc * (uint64_t)cus;
+      const char* fos = getenv("PXB_FFP_OVERSUB");    // (A/B)
+      const uint64_t over = (fos && atoi(fos) > 0 && atoi(fos) <= 64) ? (uint64_t)atoi(fos) : FF1_OVERSUB;
+      const uint64_t fres = (uint64_t)eocc * (uint64_t)cus * over;
       const unsigned fgrid = (unsigned)std::min<uint64_t>((nc + 255) / 256, fres);
       hipLaunchKernelGGL(pfn, dim3(fgrid), dim3(256), 0, st, fp);
       if (hipError_t e = hipGetLastError()) return fail(e);

@@ -383,8 +383,13 @@ struct Ff1Lane {
 
 // Grid-stride over the launch's instances, one per lane at a time; the lanes
 // of a wave run in lockstep (every instance of a skew-free batch takes the
-// same steps).  Run totals as in the per-lane event kernel: register sums,
-// wave-reduced into one of EV_TCOPIES partial rows.
+// same steps).  The grid holds several times the resident blocks
+// (pxb_run_device): a block that ends early leaves its CU to the next one, so
+// slower CUs take fewer blocks (one launch of equal static shares per
+// resident wave ran 20 % slower than two launches overlapped on two streams,
+// at every size from 2^26 to 2^29; a work queue inside the kernel spilled).
+// Run totals as in the per-lane event kernel: register sums, wave-reduced
+// into one of EV_TCOPIES partial rows.
 // (N <= 5: 5 waves per SIMD, 96 VGPRs; the compiler's own choice, 101, fits 4
 // and is 5 % slower on config 2)
 template <int N>
@@ -394,7 +399,8 @@ template <int N>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(N <= 5 ? PXB_FF1_W5 : 1))) void paxos_ff1_kernel(
     Ff1Params kp) {
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  // (wave-uniform, so kept in an SGPR: 28 B of scratch spill per lane instead of 36)
+  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
   const uint32_t n_waves = gridDim.x * (blockDim.x >> 6);
   unsigned long long* const trow = kp.part + (size_t)(wave % ev::EV_TCOPIES) * 16u;
   ev::EvTotals tot;

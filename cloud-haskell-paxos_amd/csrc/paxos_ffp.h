@@ -342,7 +342,7 @@ void paxos_ffp_kernel(FfpParams kp) {
   __shared__ uint32_t s_clog[4][LT / 2][64];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wib = threadIdx.x >> 6;
-  const uint32_t wave = blockIdx.x * (blockDim.x >> 6) + wib;
+  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * (blockDim.x >> 6) + wib));
   const uint32_t n_waves = gridDim.x * (blockDim.x >> 6);
   unsigned long long* const trow = kp.part + (size_t)(wave % ev::EV_TCOPIES) * 16u;
   ev::EvTotals tot;

@@ -381,6 +381,21 @@ def test_config5_split_list_overflow(gpu_lib, cap):
         del os.environ["PXB_EV_BAIL_CAP"]
 
 
+@pytest.mark.parametrize("c", [2, 6])
+def test_fault_free_grid_oversubscription(gpu_lib, c):
+    """The fault-free per-lane kernels run a grid of several times the
+    resident blocks (default 16): results, digests and totals are the same
+    for 1x, the default and 64x, and equal the oracle's."""
+    cfg, first, n = pxb.CONFIGS[c], 12345, 300000
+    env = "PXB_FF1_OVERSUB" if c == 2 else "PXB_FFP_OVERSUB"
+    a = pxb.run(cfg, first, n)
+    for k in ("1", "64"):
+        b = _with_env({env: k}, lambda: pxb.run(cfg, first, n))
+        assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[3] == b[3], k
+    eres, edig, _, ecnt = oracle_c.run_cpu(cfg, first, 20000, threads=THREADS)
+    assert np.array_equal(a[0][:20000], eres) and np.array_equal(a[1][:20000], edig)
+
+
 @pytest.mark.parametrize("c,n", [(1, 5000), (2, 20000), ("skew", 9000)])
 def test_ff1_bails_run_on_general_kernel(gpu_lib, c, n):
     """Fault-free single-proposer batches run one instance per lane
