@@ -145,8 +145,14 @@ int main(int argc, char** argv) {
     cfg.crash_ppm = 200000; cfg.crash_len_max = 16; cfg.crash_start_max = 8; cfg.step_cap = 256;
     if (getenv("TIGHT")) model<2, 7, 4, true, false, false, 2>(&cfg, n, rmin);   // layout 7 (tight)
     else model<2, 7, 4, true, false, false, 1>(&cfg, n, rmin);   // layout 6 (simple schedule)
+  } else if (c == 5) {
+    // the three-proposer slim shape over every instance (P <= 3 drawn per instance)
+    cfg.seed = 0x5EED0005; cfg.n_proposers = 3; cfg.n_acceptors = 9; cfg.loss_ppm = 300000;
+    cfg.delay_max = 8; cfg.crash_ppm = 200000; cfg.crash_len_max = 16; cfg.crash_start_max = 16;
+    cfg.skew_max = 3; cfg.step_cap = 512; cfg.flags = PXB_CFG_RANDOMIZE;
+    model<3, 9, 8, false, false, true>(&cfg, n, rmin);
   } else {
-    fprintf(stderr, "config 3 or 4\n");
+    fprintf(stderr, "config 3, 4 or 5\n");
     return 1;
   }
   return 0;
