@@ -92,6 +92,10 @@ struct EvKParams {
 // <= 50 (measured: 52-word lanes ran 11, the 12th block waited); 5-bit
 // entries of pool index + 1 beside the 8 Round2Success codes allow <= 23;
 // config 4 bails 0.76 % on it, host model)
+// (compact over > 16 links; tools/wave_model.cpp C5W4=1 varies it)
+#ifndef PXB_EV_CMPW_POOL
+#define PXB_EV_CMPW_POOL 48
+#endif
 #ifndef PXB_EV_SL2_POOL
 #define PXB_EV_SL2_POOL 28
 #endif
@@ -107,7 +111,7 @@ struct EvPool {
                                : (LG && PM * N <= 10)  ? PXB_EV_LG_POOL
                                : (CMP && PM * N <= 10) ? 16
                                : (PM * N <= 16)      ? (CMP ? PXB_EV_CMP_POOL : 32)
-                               : CMP                ? 48
+                               : CMP                ? PXB_EV_CMPW_POOL
                                : (PM * N <= 18)     ? (SL ? PXB_EV_SL2_POOL : 32)
                                : SL                 ? 44
                                                     : 64;
