@@ -89,7 +89,7 @@ constexpr uint32_t QWORDS = 8;          // per-slot queue / counter words (final
 // queue words: [0] the general kernel's work queue, [1] the per-lane kernel's,
 // [2] its bailed-instance count; split routing: [3] the second per-lane
 // kernel's queue, [4] its bailed-instance count
-constexpr uint32_t Q_GEN = 0, Q_EV = 1, Q_BAIL = 2, Q_EV2 = 3, Q_BAIL2 = 4;
+[[maybe_unused]] constexpr uint32_t Q_GEN = 0, Q_EV = 1, Q_BAIL = 2, Q_EV2 = 3, Q_BAIL2 = 4;   // (Q_GEN: kp.queue itself)
 
 // Sums the TCOPIES partial rows of the general kernel, and those of the
 // per-lane kernels unless the bailed-id list the general kernel ran

@@ -735,13 +735,12 @@ struct EvLane {
       const uint32_t rel = ((isR ? rtail : qtail) - b4) & (nz ? (isR ? RM : DM) : 0u);
       due_rel = d > rel ? d : rel;
       due4 = (b4 + due_rel) & 15u;
-      const bool rfull = h >= (1u << (S::IB * S::RC));
       // (as integers: a select of two booleans became five instructions)
       const uint32_t pool_out = ((pfree == 0) & !r2c) ? 1u : 0u;
       const uint32_t full = isR ? (h >> (S::IB * S::RC)) | pool_out : qlen >> 2;   // (QC = 4, qlen <= 4)
       static_assert(S::QC == 4, "request FIFOs of 4");
       bailed = bailed | (go & (full != 0u));
-      PXB_EV_PROBE(EVB_RFIFO, go & isR & rfull);
+      PXB_EV_PROBE(EVB_RFIFO, go & isR & (h >= (1u << (S::IB * S::RC))));
       PXB_EV_PROBE(EVB_POOL, go & isR & (pfree == 0) & !r2c);
       PXB_EV_PROBE(EVB_QFIFO, go & !isR & (qlen >= (uint32_t)S::QC));
       // the pool word: to a free entry (harmless unless a reply goes), or, with
