@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-5 closing pass on one GPU box: the full -m gpu suite, the profile set
 # of every bench line (tools/profile_set.sh: kernel-trace stats, SQ/GRBM,
-# FETCH_SIZE and WRITE_SIZE passes -> step.json) into profiles/r04_*, then the
+# FETCH_SIZE and WRITE_SIZE passes -> step.json) into profiles/r05_*, then the
 # default bench line, which reads those profiles: profile and bench from one box.
 # Everything also lands under gpurun_out/fin5/.
 set -o pipefail
@@ -9,6 +9,9 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R && mkdir -p gpurun_out/fin5
 timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/fin5/pytest.log 2>&1 || { tail -30 gpurun_out/fin5/pytest.log; exit 1; }
 tail -1 gpurun_out/fin5/pytest.log
+# GPU-vs-oracle fuzz over the per-lane shapes (tests/fuzz_gpu.py)
+timeout -k 10 400 python3 -u tests/fuzz_gpu.py 2000 16384 > gpurun_out/fin5/fuzz.txt 2>&1 || { tail -20 gpurun_out/fin5/fuzz.txt; exit 1; }
+tail -1 gpurun_out/fin5/fuzz.txt
 prof() {   # <config> <instances per step> <steps> <warmup>
   timeout -k 10 600 bash tools/profile_set.sh gpurun_out/fin5/config$1 $1 $2 $3 $4 || return 1
   D=gpurun_out/fin5/prof/r05_config$1; mkdir -p $D
