@@ -505,15 +505,19 @@ uint64_t pxb_canonical_bytes_nofault(uint32_t n_acceptors) { return 196ull * n_a
 
 int pxb_handoff_counts(int dev, uint64_t* out2, int reset) {
   if (!out2 || dev < 0 || dev >= 64) return PXB_E_INVAL;
-  std::lock_guard<std::mutex> lk(g_mu);
-  if (!g_slots[dev]) {
+  unsigned long long* h = nullptr;
+  {
+    // (the device wait below runs without g_mu: launches on other devices go on)
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_slots[dev]) h = g_slots[dev] + HAND_U64;
+  }
+  if (!h) {
     out2[0] = out2[1] = 0;
     return PXB_OK;
   }
   int cur = 0;
   HIPCHK(hipGetDevice(&cur));
   HIPCHK(hipSetDevice(dev));
-  unsigned long long* h = g_slots[dev] + HAND_U64;
   hipError_t e = hipDeviceSynchronize();
   if (e == hipSuccess) e = hipMemcpy(out2, h, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost);
   if (e == hipSuccess && reset) e = hipMemset(h, 0, 2 * sizeof(uint64_t));

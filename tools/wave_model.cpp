@@ -8,7 +8,7 @@
 // instruction budget per instance (profiles/r04_notes/ev_budget.txt).
 //
 //   hipcc -O2 -std=c++17 -DPXB_EV_PROBES -o /tmp/wave_model tools/wave_model.cpp
-//   /tmp/wave_model <config 3|4|5> <n_instances> [refill_min]
+//   /tmp/wave_model <config 3|4|5|7> <n_instances> [refill_min]
 //
 // refill_min > 1 models a refill that waits until that many lanes are idle
 // (or the wave has nothing else to run).
@@ -156,8 +156,14 @@ int main(int argc, char** argv) {
     } else {
       model<3, 9, 8, false, false, true>(&cfg, n, rmin);
     }
+  } else if (c == 7) {
+    // faulty log mode (pxb.LOG_FAULTY_CONFIG): the LG shape, layout 4
+    cfg.seed = 0x5EED0007; cfg.n_proposers = 2; cfg.n_acceptors = 5; cfg.loss_ppm = 100000;
+    cfg.delay_max = 4; cfg.skew_max = 3; cfg.crash_ppm = 200000; cfg.crash_len_max = 16;
+    cfg.crash_start_max = 64; cfg.step_cap = 1024; cfg.n_ticks = 16; cfg.tick_period = 8;
+    model<2, 5, 8, false, true, false>(&cfg, n, rmin);
   } else {
-    fprintf(stderr, "config 3, 4 or 5\n");
+    fprintf(stderr, "config 3, 4, 5 or 7\n");
     return 1;
   }
   return 0;
