@@ -22,6 +22,11 @@
 namespace {
 
 std::mutex g_comm_mu;
+// one pxb_run_multi at a time: concurrent calls would issue collectives on the
+// same cached communicators (and a call with another device count would
+// destroy them under the first); the per-device work inside a call is
+// parallel, so this costs a multi-device host nothing
+std::mutex g_multi_mu;
 std::vector<ncclComm_t> g_comms;   // cached communicators ...
 std::string g_comm_key;            // ... for this device list (PCI bus ids)
 
@@ -194,6 +199,7 @@ int pxb_run_multi(const pxb_config* cfg, int n_devices, pxb_result* out, uint32_
   if (hipGetDeviceCount(&visible) != hipSuccess || visible == 0) return PXB_E_NODEV;
   const int G = (n_devices <= 0) ? visible : n_devices;
   if (G > visible) return PXB_E_INVAL;
+  std::lock_guard<std::mutex> serial(g_multi_mu);
   int cur = 0;
   (void)hipGetDevice(&cur);
   HipShards b{cfg, G, out, log_digest, acc, {}, std::vector<HipShards::Dev>(G)};

@@ -172,7 +172,9 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
  * visible) by contiguous global-instance ranges, one host thread per device;
  * totals = one RCCL all-reduce (sum) of the per-device run totals over xGMI.
  * Results are identical to pxb_run for any device count (Philox is keyed by
- * the global instance id).  Replaces: Main.hs:37-53 for a multi-GPU node.     */
+ * the global instance id).  Concurrent calls from several threads run one
+ * after another (they share the cached communicators).
+ * Replaces: Main.hs:37-53 for a multi-GPU node.                               */
 int pxb_run_multi(const pxb_config* cfg, int n_devices, pxb_result* out, uint32_t* log_digest,
                   pxb_acceptor_rec* acc, pxb_counters* totals);
 

@@ -623,6 +623,35 @@ def test_run_multi_repeated_calls_release_stream_lists(gpu_lib):
         assert np.array_equal(res, want[0]) and np.array_equal(dig, want[1]) and cnt == want[3]
 
 
+def test_run_multi_concurrent_callers(gpu_lib):
+    """pxb_run_multi from four host threads at once, two configs and instance
+    ranges: the calls share the cached RCCL communicators, so the library runs
+    them one after another; every call's results and reduced totals equal its
+    single-device run."""
+    import threading
+    jobs = [(pxb.CONFIGS[3], 1000 * t, 6000) for t in range(2)] + [(pxb.CONFIGS[4], 1000 * t, 6000) for t in range(2)]
+    want = [pxb.run(cfg, f, n) for cfg, f, n in jobs]
+    got = [None] * len(jobs)
+    errs = []
+
+    def worker(i):
+        try:
+            cfg, f, n = jobs[i]
+            got[i] = pxb.run_multi(cfg, f, n)
+        except Exception as e:   # (reported by the main thread)
+            errs.append(e)
+
+    th = [threading.Thread(target=worker, args=(i,)) for i in range(len(jobs))]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errs, errs
+    for i in range(len(jobs)):
+        assert np.array_equal(got[i][0], want[i][0]) and np.array_equal(got[i][1], want[i][1])
+        assert got[i][2] == want[i][3]
+
+
 def test_stream_release_with_caller_streams(gpu_lib):
     """pxb_stream_release through the public ABI: 12 caller-created streams in
     turn (more than a device's 8 list entries), each released before the next
