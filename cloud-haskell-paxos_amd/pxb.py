@@ -166,6 +166,7 @@ def canonical_bytes_nofault(n_acceptors: int) -> int:
 
 # ---- library loading --------------------------------------------------------
 _lib = None
+ABI_VERSION = 4          # PXB_ABI_VERSION of include/paxos_batch.h this mirror binds
 
 
 class PaxosError(RuntimeError):
@@ -211,6 +212,9 @@ def load(path: str = LIB_PATH):
     lib.pxb_stream_release.restype = None
     lib.pxb_handoff_counts.argtypes = [C.c_int, vp, C.c_int]
     lib.pxb_handoff_counts.restype = C.c_int
+    if lib.pxb_abi_version() != ABI_VERSION:          # (a stale build: its struct layouts may differ)
+        raise PaxosError("libpaxos_batch.so has ABI %d, this binding expects %d — rebuild it"
+                         % (lib.pxb_abi_version(), ABI_VERSION))
     _lib = lib
     return lib
 

@@ -62,6 +62,7 @@ def test_misc_entry_points_without_gpu():
     lib = pxb.load()
     assert lib.pxb_abi_version() == 4            # 4: pxb_stream_release, pxb_handoff_counts
     assert "#define PXB_ABI_VERSION 4" in open(HEADER).read()
+    assert pxb.ABI_VERSION == 4
     # no scratch on a device yet (no GPU here): zero counts, no HIP call
     out = (C.c_uint64 * 2)(7, 7)
     assert lib.pxb_handoff_counts(0, C.cast(out, C.c_void_p), 0) == 0 and list(out) == [0, 0]
