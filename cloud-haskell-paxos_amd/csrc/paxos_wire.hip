@@ -338,25 +338,39 @@ __global__ __launch_bounds__(DTILE) void decode_kernel(const uint8_t* __restrict
   if (status) status[i] = err;
 }
 
-// scan scratch (grown on demand, one buffer per device)
+// Per-call scratch (the scans' temporary storage, the tile sums and offsets)
+// comes from a stream-ordered pool per device: allocated and freed on the
+// caller's stream, so calls on different streams never share a buffer and a
+// buffer is never freed under a kernel still using it.
 std::mutex g_mu;
-void* g_tmp[64];
-size_t g_tmp_bytes[64];
+hipMemPool_t g_pool[64];
 
 int hip_fail(hipError_t e) { return (e == hipErrorOutOfMemory) ? PXB_E_OOM : PXB_E_HIP; }
 
 unsigned tiles_of(uint64_t n, int tile) { return (unsigned)((n + tile - 1) / tile); }
 
-// per-device scratch (grown on demand)
-int scratch(int dev, size_t need) {
-  if (need <= g_tmp_bytes[dev]) return PXB_OK;
-  if (g_tmp[dev]) (void)hipFree(g_tmp[dev]);
-  g_tmp[dev] = nullptr;
-  g_tmp_bytes[dev] = 0;
-  hipError_t e = hipMalloc(&g_tmp[dev], need);
-  if (e != hipSuccess) return hip_fail(e);
-  g_tmp_bytes[dev] = need;
-  return PXB_OK;
+int scratch(int dev, size_t bytes, hipStream_t st, void** p) {
+  hipMemPool_t pool;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_pool[dev]) {
+      hipMemPoolProps props;
+      memset(&props, 0, sizeof(props));
+      props.allocType = hipMemAllocationTypePinned;
+      props.location.type = hipMemLocationTypeDevice;
+      props.location.id = dev;
+      hipError_t e = hipMemPoolCreate(&g_pool[dev], &props);
+      if (e != hipSuccess) {
+        g_pool[dev] = nullptr;
+        return hip_fail(e);
+      }
+      uint64_t keep = 64ull << 20;                       // (kept across synchronisations)
+      (void)hipMemPoolSetAttribute(g_pool[dev], hipMemPoolAttrReleaseThreshold, &keep);
+    }
+    pool = g_pool[dev];
+  }
+  hipError_t e = hipMallocFromPoolAsync(p, bytes ? bytes : 1, pool, st);
+  return (e == hipSuccess) ? PXB_OK : hip_fail(e);
 }
 
 }  // namespace pxw
@@ -365,18 +379,17 @@ using namespace pxw;
 
 extern "C" {
 
-// internal (pxb_shutdown): free the per-device scan scratch
+// internal (pxb_shutdown): destroy the per-device scratch pools
 void pxb_wire_release(void) {
   std::lock_guard<std::mutex> lk(g_mu);
   int cur = 0;
   const bool have = hipGetDevice(&cur) == hipSuccess;
   for (int d = 0; d < 64; ++d) {
-    if (!g_tmp[d]) continue;
+    if (!g_pool[d]) continue;
     (void)hipSetDevice(d);
     (void)hipDeviceSynchronize();
-    (void)hipFree(g_tmp[d]);
-    g_tmp[d] = nullptr;
-    g_tmp_bytes[d] = 0;
+    (void)hipMemPoolDestroy(g_pool[d]);
+    g_pool[d] = nullptr;
   }
   if (have) (void)hipSetDevice(cur);
 }
@@ -391,13 +404,14 @@ int pxb_wire_size(const pxb_msg* d_msgs, uint64_t count, uint32_t type, uint64_t
   // offsets[1..count] = inclusive sum of the record sizes, computed as the
   // scan reads the messages
   hipcub::TransformInputIterator<uint64_t, SizeOp, const pxb_msg*> sizes(d_msgs, SizeOp{type});
-  std::lock_guard<std::mutex> lk(g_mu);
   size_t need = 0;
   if (hipcub::DeviceScan::InclusiveSum(nullptr, need, sizes, d_offsets + 1, (int64_t)count, st) != hipSuccess)
     return PXB_E_HIP;
-  if (int rc = scratch(dev, need)) return rc;
-  size_t have = g_tmp_bytes[dev];
-  hipError_t e = hipcub::DeviceScan::InclusiveSum(g_tmp[dev], have, sizes, d_offsets + 1, (int64_t)count, st);
+  void* tmp = nullptr;
+  if (int rc = scratch(dev, need, st, &tmp)) return rc;
+  hipError_t e = hipcub::DeviceScan::InclusiveSum(tmp, need, sizes, d_offsets + 1, (int64_t)count, st);
+  const hipError_t f = hipFreeAsync(tmp, st);
+  if (e == hipSuccess) e = f;
   return (e == hipSuccess) ? PXB_OK : hip_fail(e);
 }
 
@@ -420,25 +434,28 @@ int pxb_wire_encode_all(const pxb_msg* d_msgs, uint64_t count, uint32_t type, ui
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return PXB_E_NODEV;
   const uint64_t tiles = tiles_of(count, ETILE);
-  std::lock_guard<std::mutex> lk(g_mu);
   size_t need = 0;
   if (hipcub::DeviceScan::ExclusiveSum(nullptr, need, (uint64_t*)nullptr, (uint64_t*)nullptr, (int64_t)tiles, st) !=
       hipSuccess)
     return PXB_E_HIP;
   const size_t arr = ((tiles * sizeof(uint64_t)) + 255) & ~(size_t)255;
-  if (int rc = scratch(dev, 2 * arr + need)) return rc;
-  uint64_t* tsum = reinterpret_cast<uint64_t*>(g_tmp[dev]);
-  uint64_t* toff = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(g_tmp[dev]) + arr);
-  void* tmp = reinterpret_cast<char*>(g_tmp[dev]) + 2 * arr;
+  void* buf = nullptr;
+  if (int rc = scratch(dev, 2 * arr + need, st, &buf)) return rc;
+  uint64_t* tsum = reinterpret_cast<uint64_t*>(buf);
+  uint64_t* toff = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(buf) + arr);
+  void* tmp = reinterpret_cast<char*>(buf) + 2 * arr;
   hipLaunchKernelGGL(tile_sum_kernel, dim3((unsigned)((tiles + SUM_TILES - 1) / SUM_TILES)), dim3(ETILE), 0, st, d_msgs,
                      count, type, tiles, tsum);
-  if (hipGetLastError() != hipSuccess) return PXB_E_HIP;
-  size_t have = need;
-  hipError_t e = hipcub::DeviceScan::ExclusiveSum(tmp, have, tsum, toff, (int64_t)tiles, st);
-  if (e != hipSuccess) return hip_fail(e);
-  hipLaunchKernelGGL(encode_kernel<true>, dim3((unsigned)tiles), dim3(ETILE), 0, st, d_msgs, count, type, d_offsets,
-                     toff, d_bytes);
-  return (hipGetLastError() == hipSuccess) ? PXB_OK : PXB_E_HIP;
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(tmp, need, tsum, toff, (int64_t)tiles, st);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(encode_kernel<true>, dim3((unsigned)tiles), dim3(ETILE), 0, st, d_msgs, count, type, d_offsets,
+                       toff, d_bytes);
+    e = hipGetLastError();
+  }
+  const hipError_t f = hipFreeAsync(buf, st);     // (stream-ordered: after the launches above)
+  if (e == hipSuccess) e = f;
+  return (e == hipSuccess) ? PXB_OK : hip_fail(e);
 }
 
 int pxb_wire_decode(const uint8_t* d_bytes, uint64_t n_bytes, const uint64_t* d_offsets, uint64_t count,

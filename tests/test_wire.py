@@ -188,3 +188,53 @@ def test_gpu_encode_all_matches_oracle(gpu_lib, kind, n):
     want, woffs = W.encode_batch([_as_msg(m) for m in msgs], kind)
     assert list(offs) == woffs
     assert d_b[:len(want)].cpu().numpy().tobytes() == want
+
+
+def _batch_fast(kind, n, seed):
+    """Vectorised random records (the bench's mix plus requests), for sizes the
+    per-record generator above is too slow for."""
+    rng = np.random.default_rng(seed)
+    tag = rng.integers(0, 3, n).astype(np.uint32)
+    m = np.zeros((n, 4), np.uint32)
+    m[:, 0] = tag
+    x = rng.integers(-5, 1 << 14, n).astype(np.int64).astype(np.uint32)
+    code = ((rng.integers(1, 256, n) << 24) | rng.integers(0, 1 << 24, n)).astype(np.uint32)
+    if kind == W.REQUEST:
+        m[:, 1] = x
+        m[:, 3] = np.where(tag == W.PROPOSE, code, 0)
+    else:
+        just = (tag == W.R1OK) & (rng.random(n) < 0.6)
+        m[:, 1] = np.where(tag == 2, 0, x)
+        m[:, 2] = np.where(just, rng.integers(0, 1 << 14, n), 0)
+        m[:, 3] = np.where(just, code, 0)
+    return m
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", [W.REQUEST, W.RESPONSE])
+def test_gpu_encode_all_at_scale_on_two_streams(gpu_lib, kind):
+    """pxb_wire_encode_all (tile sums, their scan, encode) equals the two-pass
+    size scan + encode (pxb_wire_size, pxb_wire_encode) at 2^22 + 17 messages,
+    on two streams at once with different batches, three times over: each
+    call's scratch (tile sums, tile offsets, scan storage) is its own,
+    allocated and freed on its stream."""
+    import torch
+    n = (1 << 22) + 17
+    batches = [_batch_fast(kind, n, 90 + kind), _batch_fast(kind, n, 91 + kind)]
+    want = [pxb.wire_encode(b, kind) for b in batches]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    bufs = []
+    for b, st in zip(batches, streams):
+        d_m = torch.from_numpy(b.view(np.int32)).cuda()
+        d_o = torch.full((n + 1,), -1, dtype=torch.int64, device="cuda")
+        d_b = torch.zeros(n * pxb.WIRE_MAX_BYTES, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
+        bufs.append((d_m, d_o, d_b, st))
+    for _ in range(3):                                  # (repeated: the pool's buffers are reused)
+        for d_m, d_o, d_b, st in bufs:
+            pxb.wire_encode_device(d_m, kind, d_o, d_b, stream=st.cuda_stream)
+    torch.cuda.synchronize()
+    for (data, offs), (_, d_o, d_b, _) in zip(want, bufs):
+        got_offs = d_o.cpu().numpy().astype(np.uint64)
+        assert np.array_equal(got_offs, offs)
+        assert d_b[:len(data)].cpu().numpy().tobytes() == data
