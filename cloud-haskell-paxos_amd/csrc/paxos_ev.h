@@ -94,7 +94,11 @@ struct Shape {
   static constexpr bool LG = LG_;                    // log mode (several Ticks, long logs; see Layouts)
   static constexpr bool SL = SL_;                    // slim 4-entry layout (see Layouts)
   static constexpr int NLQ = PM * N;                 // request (and response) links
-  static constexpr int NIN = PM * (N + 1);           // proposer-input bits (Tick + N links each)
+  // proposer-input bits: a Tick bit and N link bits per proposer (the simple
+  // schedule has no Tick after init: N link bits, so that an input bit is its
+  // response link's index)
+  static constexpr int IT = SP ? 0 : 1, IW = N + IT;
+  static constexpr int NIN = PM * IW;
   static constexpr int WW = (NLQ + NIN <= 32) ? 1 : 2;   // wheel words per slot
   static constexpr int ISH = (WW == 1) ? NLQ : 0;    // input-bit offset in its wheel word
   static constexpr int IB = POOL <= 32 ? 5 : 6;      // pool index bits
@@ -492,7 +496,7 @@ struct EvLane {
     in_mask = wi | tk;
 #pragma unroll
     for (int p = 0; p < PM; ++p) {
-      const uint32_t grp = ((1u << (N + 1)) - 1u) << (p * (N + 1));
+      const uint32_t grp = ((1u << S::IW) - 1u) << (p * S::IW);
       canon += (in_mask & grp) ? 48u : 0u;
     }
   }
@@ -861,7 +865,14 @@ struct EvLane {
   // before the acceptor part, which does not touch the pending queue).
   // (act = false: an idle lane of the wave, every op predicated off: the
   // driver runs the iteration without an exec-mask branch around it)
-  __host__ __device__ __forceinline__ bool step(const EvParams& kp, EvOut& o, bool act = true) {
+  // (fin: called with the outputs inside the step end's finishing branch,
+  // where the lane state is still live in its registers: the kernel stores
+  // the outputs there)
+  struct NoFin {
+    __host__ __device__ void operator()(const EvOut&) const {}
+  };
+  template <class Fin = NoFin>
+  __host__ __device__ __forceinline__ bool step(const EvParams& kp, EvOut& o, bool act = true, const Fin& fin = Fin()) {
     // The proposer input first, so its link and pool loads start the
     // iteration instead of waiting behind the acceptor op; a pop and an append
     // on one FIFO commute (bails may differ, and stay exact).  MI355X, 2^24
@@ -878,7 +889,7 @@ struct EvLane {
     const uint32_t ready = acc_ready_mask();
     const uint4 w0 = acc_op(kp, act, copy_ctr(), rp, ready);
     send_first(kp, w0, rp, act);
-    return end_op(kp, o, act);
+    return end_op(kp, o, act, fin);
   }
 
   // ================= ACC: one due request (Server.hs:51-78) and its reply =================
@@ -887,7 +898,18 @@ struct EvLane {
   // has copies left, only those of the acceptors it has reached (its copy to
   // acceptor a may be due now, and a takes its requests in (p, seq) order)
   __host__ __device__ __forceinline__ uint32_t acc_ready_mask() const {
+#ifdef PXB_EV_OLD_READY
     return (EARLY & pq_old) ? acc_mask & ((1u << (acur * (uint32_t)PM)) - 1u) : acc_mask;
+#else
+    // (an acceptor it has not reached takes its requests from proposers up to
+    // the broadcast's own: the copy, due now at the earliest, goes after them
+    // on its link, and links of higher proposers come after it, SEMANTICS §6)
+    // (PM = 2: all links, or the p = 0 ones, by pq's proposer bit 3 sign-extended)
+    const uint32_t cp = (pq & 31u) >> 3;
+    const uint32_t upto = (PM == 1) ? ~0u : (PM == 2) ? 0x55555555u | (uint32_t)((int32_t)(pq << 28) >> 31)
+                                                      : (cp == 0u ? 0x49249249u : cp == 1u ? 0xDB6DB6DBu : ~0u);
+    return (EARLY & pq_old) ? acc_mask & (((1u << (acur * (uint32_t)PM)) - 1u) | upto) : acc_mask;
+#endif
   }
   // (ready: acc_ready_mask(); it could be taken before this iteration's copy:
   // a request that copy makes due now belongs to an acceptor it had not reached)
@@ -995,7 +1017,7 @@ struct EvLane {
     rp.Lr = p * (uint32_t)N + a;
     rp.pw = rx | (ry << 12) | (LG ? 0u : (rz << 24)) | (rk << 30);
     rp.z = rz;
-    rp.bit = S::ISH + p * (N + 1) + 1u + a;
+    rp.bit = S::ISH + (SP ? rp.Lr : p * (N + 1) + 1u + a);
     return w1;
   }
 
@@ -1007,11 +1029,12 @@ struct EvLane {
     PXB_EV_PROBE(EVP_PROP, pin);
     {
       const uint32_t j = pin ? ctz32(in_mask) : 0u;
-      const uint32_t q = j / (uint32_t)(N + 1);
-      const uint32_t r = j - q * (uint32_t)(N + 1);
+      // (SP: bit j is response link j; j / N as a multiply-shift, exact for j < 2^10)
+      const uint32_t q = SP ? (j * ((65536u + N - 1u) / N)) >> 16 : j / (uint32_t)(N + 1);
+      const uint32_t r = SP ? 1u : j - q * (uint32_t)(N + 1);
       const bool resp = pin & (r != 0u);
       const uint32_t ra = r - 1u;
-      const uint32_t Lr = q * (uint32_t)N + (resp ? ra : 0u);
+      const uint32_t Lr = SP ? j : q * (uint32_t)N + (resp ? ra : 0u);
       const uint32_t rr = rsp_ld(Lr);
       const uint32_t rlen = (rr >> S::RL) & RLM;
       // (RH: with one entry, nk is the sentinel: rkeep tests for a second entry)
@@ -1101,7 +1124,8 @@ struct EvLane {
     const bool carry = EARLY & (pq_len == 1u) & !pq_old & ((uint32_t)s + 1u < kp.step_cap);
     return (acc_mask == 0u) & (in_mask == 0u) & ((pq_len == 0u) | carry);
   }
-  __host__ __device__ __forceinline__ bool end_op(const EvParams& kp, EvOut& o, bool act) {
+  template <class Fin = NoFin>
+  __host__ __device__ __forceinline__ bool end_op(const EvParams& kp, EvOut& o, bool act, const Fin& fin = Fin()) {
     if (act && end_ready(kp)) {
       PXB_EV_PROBE(EVP_END, true);
       // (no message in flight: every queued one falls due after s and holds a
@@ -1126,6 +1150,7 @@ struct EvLane {
       if (__builtin_expect(quiet | capped, 0)) {
         s = capped ? (int32_t)kp.step_cap - 1 : (back ? s - 1 : s);
         finish(capped, o);
+        fin(o);
         return true;
       }
       enter((int32_t)nx);

@@ -206,9 +206,13 @@ __global__ __launch_bounds__(64, CMP ? 3 : SL ? 2 : 1) void paxos_ev_kernel(EvKP
   // the crash-window draws spread over the wave, -0.3 %; grabs of as many
   // instances as idle lanes near the end of the queue, config 4 +-0,
   // configs 3 and 5 -10 % (queue-word contention).)
+  // (the refill test, taken only where the idle count changes: a refill
+  // leaves no idle lane unless the chunk drained, so it clears the flag; the
+  // loop header tests one scalar)
   uint32_t nidle = 64u;
+  bool refill = true;
   for (;;) {
-    if (nidle == 64u || (nidle >= (uint32_t)PXB_EV_REFILL_MIN && !drained)) {
+    if (refill) {
       // ---- refill idle lanes from the wave's chunk of the queue ----
       uint64_t freeb = __builtin_amdgcn_ballot_w64(L.mode == M_IDLE);
       while (freeb != 0ull && !drained) {
@@ -246,19 +250,18 @@ __global__ __launch_bounds__(64, CMP ? 3 : SL ? 2 : 1) void paxos_ev_kernel(EvKP
       const uint64_t idleb = __builtin_amdgcn_ballot_w64(L.mode == M_IDLE);
       if (idleb == ~0ull) break;                   // (drained: nothing left to run)
       nidle = (uint32_t)__popcll(idleb);
+      refill = false;                              // (nidle == 0, or drained with a live lane)
     }
 
     // ---- one iteration of every live lane ----
+    // (an ended instance's outputs and sums are taken in the step end's
+    // finishing branch, where its state is live: stored here instead, LLVM
+    // kept a copy of the acceptor registers for them in every iteration)
     EvOut o;
     bool done = false;
-    if (L.mode != M_IDLE) done = L.step(kp.p, o);
-    if (__builtin_amdgcn_ballot_w64(done | L.bailed) != 0ull) {
-      if (__builtin_expect(L.bailed, 0)) {    // beyond this kernel's capacities: re-run by the general kernel
-        const uint32_t pos = atomicAdd(kp.bail_n, 1u);
-        if (pos < kp.bail_cap) kp.bail_ids[pos] = L.gid;
-        L.mode = M_IDLE;
-        L.bailed = false;
-      } else if (done) {
+    // (an instance that bailed in its last iteration is re-run: no outputs here)
+    auto fin = [&](const EvOut& o) {
+        if (L.bailed) return;
         const uint32_t f = o.flags;
         tot.c[0] += 1u;
         tot.c[1] += (f & PXB_F_UNDECIDED) ? 1u : 0u;
@@ -285,9 +288,20 @@ __global__ __launch_bounds__(64, CMP ? 3 : SL ? 2 : 1) void paxos_ev_kernel(EvKP
             kp.acc[(uint64_t)L.gid * N + a] = make_uint4(r[0], r[1], r[2], r[3]);
           }
         }
-      }
-      nidle = (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(L.mode == M_IDLE));
+    };
+    // (iterations until some lane ends or bails: the inner loop's back edge
+    // is the one ballot)
+    do {
+      if (L.mode != M_IDLE) done = L.step(kp.p, o, true, fin);
+    } while (__builtin_amdgcn_ballot_w64(done | L.bailed) == 0ull);
+    if (__builtin_expect(L.bailed, 0)) {      // beyond this kernel's capacities: re-run by the general kernel
+      const uint32_t pos = atomicAdd(kp.bail_n, 1u);
+      if (pos < kp.bail_cap) kp.bail_ids[pos] = L.gid;
+      L.mode = M_IDLE;
+      L.bailed = false;
     }
+    nidle = (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(L.mode == M_IDLE));
+    refill = nidle == 64u || (nidle >= (uint32_t)PXB_EV_REFILL_MIN && !drained);
   }
 #ifdef PXB_WAVE_TIMES
   if (kp.dbg && blockIdx.x < 65536u) {
