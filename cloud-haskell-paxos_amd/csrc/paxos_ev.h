@@ -1066,6 +1066,58 @@ struct EvLane {
       } else {
         MV = w1 & 3u, C2 = (w1 >> 2) & 3u, CM = (w1 >> 4) & 3u;
       }
+#ifndef PXB_EV_OLD_PROP
+      if constexpr (!LG) {
+        // The handlers as whole-word updates of the packed state (one select
+        // among the few outcomes, not a select per field); the same
+        // transitions as the field form below (Client.hs:128-207)
+        const uint32_t maj = (uint32_t)N >> 1;        // haveMajority: acks > floor(N/2), :191-194
+        const uint32_t key = (pin ? ((!SP && r == 0u) ? 3u : rkind) : 4u) * 4u + R;
+        const bool t_go = !SP && key == 3u * 4u + IDLE;                  // handleTick, :196-207
+        const bool h_go = (key - (HAVE * 4u + ROUND1) < 2u) & (px >= T);  // HaveTicket, :128-140
+        const bool o_go = (key == R1OK * 4u + ROUND1) & (T == px);        // Round1OK, :142-170
+        const bool s_go = key == R2S * 4u + ROUND2;                      // Round2Success, :172-189 (Q2)
+        const bool maj1 = K >= maj;                                      // acks + 1 > maj
+        const bool o_take = (MV == 0u) | ((pz != 0u) & !(MT >= py));     // MostRecent (Common.hs:61-65)
+        const uint32_t mv = o_take ? pz : MV;
+        const bool o_maj = o_go & maj1, s_maj = s_go & maj1;
+        const uint32_t PDb = w0 & (1u << 30);
+        const bool sPD = s_maj & (PDb != 0u);                            // Execute + restart (:185)
+        const bool ask = t_go | h_go;
+        const bool restart = ask | sPD;                                  // -> Round1 with a new ticket
+        const uint32_t Tn = (h_go ? px : T) + (restart ? 1u : 0u);
+        const uint32_t C2n = o_maj ? ((mv == 0u) ? CM : mv) : C2;        // Q5: pending whenever mr is Just
+        // pw0: restart: Tn, Round1, acks 0, mr_t 0, pending kept; Round2 entry:
+        // T, acks 0, mr_t 0, pending = mr is Just; done (Idle): T and mr_t kept;
+        // an ack below the majority: acks + 1 (Round1OK: mr_t := the MostRecent ticket)
+        // (candidates first, then selects of plain values: clang emits a
+        // conditional operator over larger expressions as branches)
+        const uint32_t dmt = (py - MT) << 12;
+        const uint32_t inc = (1u << 24) + ((o_go & o_take) ? dmt : 0u);
+        const uint32_t pdo = (mv != 0u) ? 1u << 30 : 0u;
+        const uint32_t c_rs = Tn | (ROUND1 << 28) | PDb, c_om = T | (ROUND2 << 28) | pdo;
+        const uint32_t c_sd = w0 & 0xFFFFFFu, c_in = w0 + inc;
+        uint32_t w0n = (o_go | s_go) ? c_in : w0;
+        w0n = s_maj ? c_sd : w0n;
+        w0n = o_maj ? c_om : w0n;
+        w0n = restart ? c_rs : w0n;
+        // pw1: mr_v := 0 (restart, Round2 entry) or the MostRecent value (an ack
+        // below the majority); r2_v := C2n on Round2 entry; cmd := 0 when done,
+        // c<id> on a Tick
+        const uint32_t tick_cm = SP ? 0u : ((q + 1u) << 4);
+        const uint32_t c1_rs = (t_go ? (w1 & 0xCu) | tick_cm : w1 & ~3u), c1_om = (w1 & 0x30u) | (C2n << 2);
+        const uint32_t c1_ok = (w1 & ~3u) | mv, c1_sd = w1 & 0xFu;
+        uint32_t w1n = s_maj ? c1_sd : w1;
+        w1n = o_go ? c1_ok : w1n;
+        w1n = o_maj ? c1_om : w1n;
+        w1n = restart ? c1_rs : w1n;
+        put(pw0, q, w0n);
+        put(pw1, q, w1n);
+        const uint32_t k0o = ask ? ASK : o_maj ? PROPOSE : s_maj ? EXECUTE : NONE;
+        broadcast(q, k0o, ask ? Tn : T, C2n, k0o != NONE, Tn, sPD, C2n);
+        return;
+      }
+#endif
       uint32_t k0o = NONE, x0o = 0, z0o = 0;
       bool b1 = false;                                // the restart's AskForTicket (Client.hs:185)
       const uint32_t maj = (uint32_t)N >> 1;          // haveMajority: acks > floor(N/2), :191-194

@@ -189,10 +189,13 @@ def main() -> None:
             row.append("%6s" % ("" if v + sa == 0 else "%d/%d" % (v, sa)))
         print("%-10s %3d %5d  " % (lab, depth, n) + " ".join("%14s" % r for r in row))
     print("\n(cells: VALU/SALU)")
-    print("\nper section over all depth-1 blocks (static), by helper:")
+    # (the iteration's loop depth: 1, or 2 since the step loop nests in the
+    # refill loop; BUDGET_DEPTH overrides)
+    loop_depth = int(os.environ.get("BUDGET_DEPTH", "2" if any(d == 2 and "prop_op" in str(c) for _, d, _, c in per_block) else "1"))
+    print("\nper section over all depth-%d blocks (static), by helper:" % loop_depth)
     tot = collections.Counter()
     for lab, depth, n, c in per_block:
-        if depth == 1:
+        if depth == loop_depth:
             tot.update(c)
     for s in secs:
         items = {(h, kl): k for (sc, h, kl), k in tot.items() if sc == s}
