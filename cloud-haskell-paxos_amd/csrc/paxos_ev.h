@@ -317,7 +317,18 @@ struct EvLane {
   uint32_t accv[LG ? N : 1];          // LG: the stored command and log length of each acceptor
   uint32_t rseqv[SL ? (NLQ + 3) / 4 : 1];   // SL: the reply seqs, a byte per request link
   uint32_t pq, pq_len, acur;          // pending broadcasts (p << 3 | slot, 5 bits each), next acceptor
-  bool pq_old;                        // the head pending broadcast was made at step s - 1
+  // pending broadcasts at the head of pq made at step s - 1 (carried over by
+  // end_op: at most one, or two on the simple schedule, CARRY2)
+  // (CARRY2, opt-in: two broadcasts carried over on the simple schedule.
+  // Host model, config 4: 0.4 % fewer iterations -- the carried copies then
+  // hold up the next step instead -- for 5 more VALU per iteration: not used)
+#ifdef PXB_EV_CARRY2
+  static constexpr bool CARRY2 = SP && EARLY;
+#else
+  static constexpr bool CARRY2 = false;
+#endif
+  // (a count only with CARRY2: a lane-mask bool is one scalar op to update)
+  typename std::conditional<CARRY2, uint32_t, bool>::type pqo;
   uint32_t canon0;                    // canon on entering a step that carries one over (else canon - 1)
   pool_mask_t pfree;                  // free response-pool words
   uint32_t lflags, rounds, dval, dtick, execs, msgs, canon;   // (msgs: the replies; see msgs_sent)
@@ -465,8 +476,8 @@ struct EvLane {
   // 48 canonical bytes per proposer with an input (SEMANTICS §8)
   __host__ __device__ __forceinline__ void enter(int32_t t) {
     s = t;
-    pq_old = pq_len != 0u;                           // (only ever one: end_op)
-    if constexpr (!SP) canon0 = pq_old ? canon : canon - 1u;   // (SP: see end_op)
+    pqo = CARRY2 ? pq_len : (pq_len != 0u);          // (at most one, CARRY2 two: end_op)
+    if constexpr (!SP) canon0 = pqo ? canon : canon - 1u;   // (SP: see end_op)
     const uint32_t slot = (uint32_t)t & WM;
     uint32_t wq, wi;
     if (S::WW == 1) {
@@ -596,7 +607,7 @@ struct EvLane {
 #pragma unroll
     for (int i = 0; i < W * S::WW; ++i) m.st(S::WHEEL + i, 0u);
     pq = pq_len = acur = 0u;
-    pq_old = false;
+    pqo = 0;
     pfree = full_pool();
     lflags = rounds = dval = dtick = execs = msgs = canon = 0u;
     clog = 0ull;
@@ -686,7 +697,7 @@ struct EvLane {
                                                      bool act = true) {
     const bool isR = rp.snd;                         // (only with act: acc_op)
     // the copy's bookkeeping (as in copy_send)
-    const uint32_t sb = (uint32_t)s - (pq_old ? 1u : 0u);
+    const uint32_t sb = (uint32_t)s - (pqo ? 1u : 0u);
     const bool csnd = act & !isR & (pq_len != 0u);
     const uint32_t ce = pq & 31u;
     const uint32_t cp = ce >> 3, cslot = ce & 7u, ca = acur;
@@ -697,7 +708,8 @@ struct EvLane {
       acur = wrap ? 0u : (csnd ? a1 : acur);
       pq = wrap ? pq >> 5 : pq;
       pq_len -= wrap ? 1u : 0u;
-      pq_old = pq_old & !wrap;
+      if constexpr (CARRY2) pqo -= (wrap & (pqo != 0u)) ? 1u : 0u;
+      else pqo = pqo & !wrap;
       put(nsent, cp, ck + (wrap ? 1u : 0u));
     }
     const bool snd = isR | csnd;
@@ -815,7 +827,7 @@ struct EvLane {
   }
   __host__ __device__ __forceinline__ void copy_send(const EvParams& kp, bool act, const uint4& w) {
     // the broadcast's own step: s, or s - 1 for one carried over by end_op
-    const uint32_t sb = (uint32_t)s - (pq_old ? 1u : 0u);
+    const uint32_t sb = (uint32_t)s - (pqo ? 1u : 0u);
     const uint32_t s4 = sb & 15u;
     const bool snd = act & (pq_len != 0u);
     PXB_EV_PROBE(EVP_COPY, snd);
@@ -828,7 +840,8 @@ struct EvLane {
       acur = wrap ? 0u : (snd ? a1 : acur);
       pq = wrap ? pq >> 5 : pq;
       pq_len -= wrap ? 1u : 0u;
-      pq_old = pq_old & !wrap;
+      if constexpr (CARRY2) pqo -= (wrap & (pqo != 0u)) ? 1u : 0u;
+      else pqo = pqo & !wrap;
       put(nsent, cp, ck + (wrap ? 1u : 0u));
     }
     // (w: the draw of copy_ctr() taken before this call)
@@ -899,7 +912,7 @@ struct EvLane {
   // acceptor a may be due now, and a takes its requests in (p, seq) order)
   __host__ __device__ __forceinline__ uint32_t acc_ready_mask() const {
 #ifdef PXB_EV_OLD_READY
-    return (EARLY & pq_old) ? acc_mask & ((1u << (acur * (uint32_t)PM)) - 1u) : acc_mask;
+    return (EARLY & (pqo != 0)) ? acc_mask & ((1u << (acur * (uint32_t)PM)) - 1u) : acc_mask;
 #else
     // (an acceptor it has not reached takes its requests from proposers up to
     // the broadcast's own: the copy, due now at the earliest, goes after them
@@ -908,7 +921,16 @@ struct EvLane {
     const uint32_t cp = (pq & 31u) >> 3;
     const uint32_t upto = (PM == 1) ? ~0u : (PM == 2) ? 0x55555555u | (uint32_t)((int32_t)(pq << 28) >> 31)
                                                       : (cp == 0u ? 0x49249249u : cp == 1u ? 0xDB6DB6DBu : ~0u);
-    return (EARLY & pq_old) ? acc_mask & (((1u << (acur * (uint32_t)PM)) - 1u) | upto) : acc_mask;
+    uint32_t ok = ((1u << (acur * (uint32_t)PM)) - 1u) | upto;
+    if constexpr (CARRY2) {
+      // (a second carried broadcast, whose copies all wait: no acceptor takes
+      // requests of proposers above its own)
+      const uint32_t c2 = (pq >> 8) & 3u;
+      const uint32_t upto2 = (PM == 1) ? ~0u : (PM == 2) ? 0x55555555u | (uint32_t)((int32_t)(pq << 23) >> 31)
+                                                         : (c2 == 0u ? 0x49249249u : c2 == 1u ? 0xDB6DB6DBu : ~0u);
+      ok &= ((uint32_t)pqo > 1u) ? upto2 : ~0u;
+    }
+    return (EARLY & (pqo != 0)) ? acc_mask & ok : acc_mask;
 #endif
   }
   // (ready: acc_ready_mask(); it could be taken before this iteration's copy:
@@ -993,11 +1015,33 @@ struct EvLane {
       log_len += 1u;
     }
     // (a lane without a live request rebuilds its old word unchanged)
+    uint32_t pw;                                     // the reply's response word
     if constexpr (LG) {
       put(accw, a, nt_max | (nt_store << 12) | ((dead | panic) ? (1u << A_DEAD) : 0u));
       put(accv, a, nval | (log_len << A_LEN));
+      pw = rx | (ry << 12) | (rk << 30);
     } else {
+#ifdef PXB_EV_OLD_ACC
       put(accw, a, nt_max | (nt_store << 12) | (nval << 24) | ((dead | panic) ? (1u << 26) : 0u) | (log_len << 27));
+      pw = rx | (ry << 12) | (rz << 24) | (rk << 30);
+#else
+      // whole-word updates (candidates, then selects of plain values): grant
+      // sets t_max; accept sets t_store and val; Execute clears them and
+      // appends (log length + 1; a 32nd entry bailed above); panic sets dead.
+      // A Round1OK carries (x, t_store, val), which sit in the reply's fields
+      // at their acceptor-word offsets.
+      const uint32_t c_gr = (A & ~0xFFFu) | x, c_ac = (A & 0xFC000FFFu) | (x << 12) | (z << 24);
+      const uint32_t c_rn = (A & 0xFC000FFFu) + (1u << 27), c_pn = A | (1u << 26);
+      uint32_t An = panic ? c_pn : A;
+      An = run ? c_rn : An;
+      An = accept ? c_ac : An;
+      An = grant ? c_gr : An;
+      put(accw, a, An);
+      const uint32_t p_gr = x | (A & 0x03FFF000u) | (R1OK << 30), p_hv = (A & 0xFFFu) | (HAVE << 30);
+      constexpr uint32_t p_ac = R2S << 30;
+      pw = accept ? p_ac : p_hv;
+      pw = grant ? p_gr : pw;
+#endif
     }
     const bool snd1 = live & !is_exec;              // the reply, on link a -> p
     m.st(S::REQ + L, acc ? rq2 + ((S::CMP && snd1) ? 1u << S::KSH : 0u) : wq);
@@ -1015,7 +1059,7 @@ struct EvLane {
     else if constexpr (!S::CMP) m.st16(S::RSEQ, L, snd1 ? kr + 1u : kr);
     rp.snd = snd1;
     rp.Lr = p * (uint32_t)N + a;
-    rp.pw = rx | (ry << 12) | (LG ? 0u : (rz << 24)) | (rk << 30);
+    rp.pw = pw;
     rp.z = rz;
     rp.bit = S::ISH + (SP ? rp.Lr : p * (N + 1) + 1u + a);
     return w1;
@@ -1173,7 +1217,9 @@ struct EvLane {
   // delays are counted from s, so none is due before s + 1.
   __host__ __device__ __forceinline__ bool end_ready(const EvParams& kp) const {
     // (non-short-circuit: && / || here became a tree of exec-mask branches)
-    const bool carry = EARLY & (pq_len == 1u) & !pq_old & ((uint32_t)s + 1u < kp.step_cap);
+    // (CARRY2: the copies of two broadcasts of this step; a carried broadcast
+    // is never carried again: its copies' delays count from its own step)
+    const bool carry = EARLY & (pq_len <= (CARRY2 ? 2u : 1u)) & !pqo & ((uint32_t)s + 1u < kp.step_cap);
     return (acc_mask == 0u) & (in_mask == 0u) & ((pq_len == 0u) | carry);
   }
   template <class Fin = NoFin>
