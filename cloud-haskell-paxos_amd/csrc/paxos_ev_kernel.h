@@ -200,15 +200,16 @@ __global__ __launch_bounds__(64, CMP ? 3 : SL ? 2 : 1) void paxos_ev_kernel(EvKP
   // several, and a lane ends every ~17 wave-iterations (config 4), so nearly
   // every refill started one lane; waiting for a second costs each instance
   // ~8 idle lane-iterations of its ~1090 (tools/wave_model.cpp refill_min):
-  // MI355X A/B, config 4 at 2^24: +1.3 %.  The per-iteration refill test is
-  // one scalar compare.  (Measured and not kept, profiles/r04_notes: idle
-  // lanes running the iteration predicated off instead of masked, -0.9 %;
-  // the crash-window draws spread over the wave, -0.3 %; grabs of as many
-  // instances as idle lanes near the end of the queue, config 4 +-0,
-  // configs 3 and 5 -10 % (queue-word contention).)
-  // (the refill test, taken only where the idle count changes: a refill
-  // leaves no idle lane unless the chunk drained, so it clears the flag; the
-  // loop header tests one scalar)
+  // MI355X A/B, config 4 at 2^24: +1.3 %.  The refill test is taken only
+  // where the idle count changes (a refill leaves no idle lane unless the
+  // chunk drained, so it clears the flag), and the steps in between run in an
+  // inner loop whose back edge is one ballot (round 5: with the outputs stored
+  // in the finishing branch, config 4 +3.4 %).  (Measured and not kept,
+  // profiles/r04_notes: idle lanes running the iteration predicated off
+  // instead of masked, -0.9 %; the crash-window draws spread over the wave,
+  // -0.3 %; grabs of as many instances as idle lanes near the end of the
+  // queue, config 4 +-0, configs 3 and 5 -10 % (queue-word contention); a
+  // 2x-unrolled step loop spills.)
   uint32_t nidle = 64u;
   bool refill = true;
   for (;;) {
