@@ -656,13 +656,19 @@ struct EvLane {
     PXB_EV_PROBE(EVB_RING, (p0 & (ref_nib(q, slot0) != 0u)) | (p1 & (ref_nib(q, slot1) != 0u)));
     PXB_EV_PROBE(EVP_BCAST, p0);
     if (p0) {                                        // (p1 only with p0)
-      if constexpr (LG) {
+      if constexpr (LG && !PXB_EV_STORE_BACK) {
         m.st(S::BRING + q * S::BR + slot0, x0 | (z0 << 12) | (kind0 << 30));
         if (p1) m.st(S::BRING + q * S::BR + slot1, x1 | (ASK << 30));
-      } else if constexpr (!PXB_EV_STORE_BACK) {
+      } else if constexpr (!LG && !PXB_EV_STORE_BACK) {
         m.st16h(S::BRING + bring_word(q, slot0), bring_half(q, slot0), x0 | (z0 << 12) | (kind0 << 14));
         if (p1) m.st16h(S::BRING + bring_word(q, slot1), bring_half(q, slot1), x1 | (ASK << 14));
       }
+    }
+    if constexpr (LG && PXB_EV_STORE_BACK) {       // (the same with the log mode's payload words)
+      const uint32_t w0a = S::BRING + q * S::BR + slot0, w1a = S::BRING + q * S::BR + slot1;
+      const uint32_t o0 = m.ld(w0a), o1 = m.ld(w1a);
+      m.st(w0a, p0 ? x0 | (z0 << 12) | (kind0 << 30) : o0);
+      m.st(w1a, p1 ? x1 | (ASK << 30) : o1);
     }
     if constexpr (!LG && PXB_EV_STORE_BACK) {
       // (without a branch: a lane that makes no broadcast stores the slots'
@@ -784,13 +790,22 @@ struct EvLane {
         rlen = (wv >> S::RL) & RLM;
         rtail = (wv >> S::RD) & 15u;
       }
-      const uint32_t len = isR ? rlen : (wv >> S::QL) & QLM;
+      // (both links' fields in plain variables, then selects: clang made the
+      // selects over expressions branches, with the tail's pool load inside)
+      const uint32_t qlen = (wv >> S::QL) & QLM;
       // (a request entry's due is mod 2^DB: every queued due lies within 2^DB of the send step)
-      const uint32_t tail = isR ? rtail : (wv >> (((uint32_t)S::EB * len - (uint32_t)S::DB) & 31u)) & DM;
-      const uint32_t rel = (tail - b4) & (len ? (isR ? 15u : DM) : 0u);
+      const uint32_t qtail = (wv >> (((uint32_t)S::EB * qlen - (uint32_t)S::DB) & 31u)) & DM;
+      const uint32_t len = isR ? rlen : qlen;
+      const uint32_t tail = isR ? rtail : qtail;
+      const uint32_t lm = isR ? 15u : DM;
+      const uint32_t rel = (tail - b4) & (len ? lm : 0u);
       due_rel = d > rel ? d : rel;
       due4 = (b4 + due_rel) & 15u;
-      bailed = bailed | (go & (isR ? (len >= (uint32_t)S::RC) | ((pfree == 0) & !r2c) : (len >= (uint32_t)S::QC)));
+      // (as integers, as in the halfword path)
+      const uint32_t pool_out = ((pfree == 0) & !r2c) ? 1u : 0u;
+      const uint32_t rfull = (rlen >= (uint32_t)S::RC) ? 1u : 0u, qfull = (qlen >= (uint32_t)S::QC) ? 1u : 0u;
+      const uint32_t full = isR ? rfull | pool_out : qfull;
+      bailed = bailed | (go & (full != 0u));
       PXB_EV_PROBE(EVB_RFIFO, go & isR & (len >= (uint32_t)S::RC));
       PXB_EV_PROBE(EVB_POOL, go & isR & (pfree == 0) & !r2c);
       PXB_EV_PROBE(EVB_QFIFO, go & !isR & (len >= (uint32_t)S::QC));
