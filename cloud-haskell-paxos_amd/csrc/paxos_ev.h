@@ -249,6 +249,13 @@ extern thread_local uint32_t ev_probe_bits;
 #define PXB_EV_PROBE(b, c) ((void)0)
 #endif
 
+// (a small index times a constant: the 24-bit mask lets LLVM use
+// v_mad_u32_u24 / v_mul_u32_u24, full rate, where it cannot bound the operand
+// itself -- it had emitted v_mad_u64_u32 and v_mul_lo_u32)
+__host__ __device__ __forceinline__ uint32_t u24(uint32_t x) { return x & 0xFFFFFFu; }
+// x * C: a shift for a power of two (where the mask only costs), else the 24-bit form
+template <uint32_t C>
+__host__ __device__ __forceinline__ uint32_t mulc(uint32_t x) { return ((C & (C - 1u)) == 0u) ? x * C : u24(x) * C; }
 __host__ __device__ __forceinline__ uint32_t ctz32(uint32_t x) { return x ? (uint32_t)__builtin_ctz(x) : 32u; }
 __host__ __device__ __forceinline__ uint32_t popc32(uint32_t x) { return (uint32_t)__builtin_popcount(x); }
 __host__ __device__ __forceinline__ uint32_t nbits32(uint32_t x) { return x ? 32u - (uint32_t)__builtin_clz(x) : 0u; }
@@ -725,7 +732,7 @@ struct EvLane {
     const bool go = snd & ok;
     const uint32_t base = isR ? (uint32_t)s : sb;   // the send step (a carried copy's is s - 1)
     const uint32_t b4 = base & 15u;
-    const uint32_t Lq = ca * (uint32_t)PM + cp;
+    const uint32_t Lq = mulc<PM>(ca) + cp;
     // (a Round2Success in a compact link word needs no pool word)
     const bool r2c = S::RCODE & isR & ((rp.pw >> 30) == R2S);
     const uint32_t k2 = (POOL > 32) ? (uint32_t)__builtin_ctzll((unsigned long long)pfree | (1ull << 63))
@@ -864,7 +871,7 @@ struct EvLane {
     const uint32_t d = 1u + mulhi_n(w.y, dmax);      // (delay_max <= 1: always 1)
     // enqueue (predicated: inactive lanes store to the dummy word)
     const bool go = snd & ok;
-    const uint32_t Lq = ca * (uint32_t)PM + cp;
+    const uint32_t Lq = mulc<PM>(ca) + cp;
     const uint32_t wq = m.ld(S::REQ + Lq);
     const uint32_t qlen = (wq >> S::QL) & QLM;
     bailed = bailed | (go & (qlen >= (uint32_t)S::QC));
@@ -1079,7 +1086,7 @@ struct EvLane {
     rp.Lr = p * (uint32_t)N + a;
     rp.pw = pw;
     rp.z = rz;
-    rp.bit = S::ISH + (SP ? rp.Lr : p * (N + 1) + 1u + a);
+    rp.bit = S::ISH + (SP ? rp.Lr : mulc<N + 1>(p) + 1u + a);
     return w1;
   }
 
@@ -1093,10 +1100,10 @@ struct EvLane {
       const uint32_t j = pin ? ctz32(in_mask) : 0u;
       // (SP: bit j is response link j; j / N as a multiply-shift, exact for j < 2^10)
       const uint32_t q = SP ? (j * ((65536u + N - 1u) / N)) >> 16 : j / (uint32_t)(N + 1);
-      const uint32_t r = SP ? 1u : j - q * (uint32_t)(N + 1);
+      const uint32_t r = SP ? 1u : j - mulc<N + 1>(q);
       const bool resp = pin & (r != 0u);
       const uint32_t ra = r - 1u;
-      const uint32_t Lr = SP ? j : q * (uint32_t)N + (resp ? ra : 0u);
+      const uint32_t Lr = SP ? j : mulc<N>(q) + (resp ? ra : 0u);
       const uint32_t rr = rsp_ld(Lr);
       const uint32_t rlen = (rr >> S::RL) & RLM;
       // (RH: with one entry, nk is the sentinel: rkeep tests for a second entry)
