@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 5 (final code): where the tight kernel's waves' cycles go, config 4 at 2^24;
+# Round 5 (final code): where the per-lane waves' cycles go (PMC_CONFIG, PMC_N: default config 4 at 2^24);
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p $R/gpurun_out/r05pmc2
@@ -10,7 +10,7 @@ for tag in tight; do
   if [ $tag = l6 ]; then export PXB_NO_TIGHT=1; else unset PXB_NO_TIGHT; fi
   for pass in 1 2; do
     C=$P1; [ $pass = 2 ] && C=$P2
-    timeout -s KILL 120 rocprofv3 --pmc $C -d $R/gpurun_out/r05pmc2/$tag$pass -o pmc --output-format csv -- python3 $R/bench.py --config 4 --instances 16777216 --steps 1 --warmup 1 --no-cpu --no-extra --one-stream > $R/gpurun_out/r05pmc2/$tag$pass.log 2>&1 || { tail -5 $R/gpurun_out/r05pmc2/$tag$pass.log; exit 1; }
+    timeout -s KILL 120 rocprofv3 --pmc $C -d $R/gpurun_out/r05pmc2/$tag$pass -o pmc --output-format csv -- python3 $R/bench.py --config ${PMC_CONFIG:-4} --instances ${PMC_N:-16777216} --steps 1 --warmup 1 --no-cpu --no-extra --one-stream > $R/gpurun_out/r05pmc2/$tag$pass.log 2>&1 || { tail -5 $R/gpurun_out/r05pmc2/$tag$pass.log; exit 1; }
   done
 done
 cd $R && python3 - <<'PY'
