@@ -322,7 +322,12 @@ struct EvLane {
   // acceptor states (Server.hs:24-31), isolation windows, log digests
   uint32_t accw[N], win[N], accd[N];
   uint32_t accv[LG ? N : 1];          // LG: the stored command and log length of each acceptor
-  uint32_t rseqv[SL ? (NLQ + 3) / 4 : 1];   // SL: the reply seqs, a byte per request link
+  // SL: the reply seqs, a byte per request link: four links a word, or (RSA:
+  // three proposers) a word per acceptor, byte p, so that the selects share the
+  // acceptor's one-hot masks with its state words (2 VGPRs more)
+  static constexpr bool RSA = SL && PM == 3;
+  static constexpr int NRS = RSA ? N : (NLQ + 3) / 4;
+  uint32_t rseqv[SL ? NRS : 1];
   uint32_t pq, pq_len, acur;          // pending broadcasts (p << 3 | slot, 5 bits each), next acceptor
   // pending broadcasts at the head of pq made at step s - 1 (carried over by
   // end_op: at most one, or two on the simple schedule, CARRY2)
@@ -620,7 +625,7 @@ struct EvLane {
     }
     if constexpr (SL) {
 #pragma unroll
-      for (int i = 0; i < (int)((NLQ + 3) / 4); ++i) rseqv[i] = 0u;
+      for (int i = 0; i < NRS; ++i) rseqv[i] = 0u;
     }
 #pragma unroll
     for (int i = 0; i < W * S::WW; ++i) m.st(S::WHEEL + i, 0u);
@@ -977,8 +982,9 @@ struct EvLane {
     const uint32_t a = L / (uint32_t)PM, p = L - a * (uint32_t)PM;
     const uint32_t wq = m.ld(S::REQ + L);
     // the reply's link sequence number
-    const uint32_t kw = SL ? get(rseqv, L >> 2) : 0u;
-    const uint32_t kr = S::CMP ? (wq >> S::KSH) : SL ? (kw >> (8u * (L & 3u))) & 0xFFu : m.ld16(S::RSEQ, L);
+    const uint32_t kw = SL ? get(rseqv, RSA ? a : L >> 2) : 0u;
+    const uint32_t ksh = 8u * (RSA ? p : (L & 3u));   // (its byte)
+    const uint32_t kr = S::CMP ? (wq >> S::KSH) : SL ? (kw >> ksh) & 0xFFu : m.ld16(S::RSEQ, L);
     const uint32_t len = (wq >> S::QL) & QLM;
     const uint32_t bslot = wq & ((1u << S::SB) - 1u);
     // the popped word: entries shifted down one, length - 1 (fields above the
@@ -1091,7 +1097,7 @@ struct EvLane {
     msgs += snd1 ? 1u : 0u;
     bailed = bailed | (snd1 & (kr == (S::CMP ? (1u << S::KB) - 1u : SL ? 0xFFu : 0xFFFFu)));
     PXB_EV_PROBE(EVB_RSEQ, snd1 & (kr == (S::CMP ? (1u << S::KB) - 1u : SL ? 0xFFu : 0xFFFFu)));
-    if constexpr (SL) put(rseqv, L >> 2, kw + (snd1 ? 1u << (8u * (L & 3u)) : 0u));
+    if constexpr (SL) put(rseqv, RSA ? a : L >> 2, kw + (snd1 ? 1u << ksh : 0u));
     else if constexpr (!S::CMP) m.st16(S::RSEQ, L, snd1 ? kr + 1u : kr);
     rp.snd = snd1;
     rp.Lr = p * (uint32_t)N + a;
