@@ -417,11 +417,8 @@ def log_faulty_line(stream, dev, n=1 << 22, general=True):
             "commands_committed_per_s": ecnt["executes"] / es, "kernel_ms": ek,
             "roofline": roofline("config7", n, ek, ecnt["canon_bytes"] / 2), "counters": ecnt}
     if general:
-        os.environ["PXB_NO_EV"] = "1"
-        try:
+        with pxb.hooks(PXB_NO_EV="1"):
             gs, gk, gcnt = run_workload(GpuLeg(cfg, n, 0, 1, stream, dev), n, 2, 1, 1)
-        finally:
-            del os.environ["PXB_NO_EV"]
         assert gcnt == ecnt, (gcnt, ecnt)
         line["general_kernel"] = {"instances_per_s": gcnt["instances"] / gs, "kernel_ms": gk}
         line["speedup_vs_general_kernel"] = gk / ek

@@ -121,6 +121,14 @@ __global__ __launch_bounds__(TCOPIES) void finalize_kernel(unsigned long long* p
   if (t >= 16 && t < 16 + QWORDS) queue[t - 16] = 0u;
 }
 
+// the device's hand-off counts read (pxb_handoff_counts) of the device's hand-off counts (pxb_handoff_counts):
+// out[t] = the count, zeroed in the same atomic when reset, so a finalize_kernel
+// of another thread's chunk never adds between the read and the zeroing
+__global__ void hand_xchg_kernel(unsigned long long* h, unsigned long long* out, int reset) {
+  const uint32_t t = threadIdx.x;
+  if (t < 2) out[t] = reset ? atomicExch(&h[t], 0ull) : atomicAdd(&h[t], 0ull);
+}
+
 // ---- host side ----------------------------------------------------------------
 typedef void (*kernel_ptr)(KParams);
 typedef void (*ev_kernel_ptr)(ev::EvKParams);
@@ -246,6 +254,21 @@ static kernel_fn pick(uint32_t pm, uint32_t n, bool logm, bool ff) {
   return kernel_fn{nullptr, 0, 0};
 }
 
+// Test and A/B hooks (environment variables), read once -- on the first
+// launch, or by pxb_reload_hooks() -- and never by getenv in the launch path,
+// which is not safe against a concurrent setenv (tests/conftest.py's
+// `hooks` helper sets them and reloads)
+struct Hooks {
+  bool no_ev, no_ff1, no_ffp, no_split, no_tight, fail_after_first, ff1_bail;
+  int bail_cap;                   // PXB_EV_BAIL_CAP (-1: the default)
+  int blocks_per_cu;              // PXB_BLOCKS_PER_CU (0: none)
+  int ff1_oversub, ffp_oversub;   // PXB_FF1_OVERSUB / PXB_FFP_OVERSUB (0: FF1_OVERSUB)
+  char multi_fail_phase[16];      // PXB_MULTI_FAIL_PHASE / _DEVICE (paxos_multi.cpp)
+  int multi_fail_device;
+};
+static Hooks g_hooks;
+static bool g_hooks_read = false;
+
 static thread_local int g_last_hip = 0;
 #ifdef PXB_STAMPS
 static unsigned long long* g_dbg = nullptr;
@@ -266,6 +289,16 @@ constexpr size_t SLOT_U64 = 2 * ROWS_U64 + 16;
 constexpr size_t HAND_U64 = (size_t)QSLOTS * SLOT_U64;
 static unsigned long long* g_slots[64];
 static uint32_t g_qseq[64];
+// Each slot's event is recorded behind the last chunk that used it (its
+// finalize_kernel, or the zeroing of a failed chunk), and a chunk that takes
+// the slot makes its stream wait for it (hipStreamWaitEvent, on the device),
+// so a 65th chunk in flight across streams waits for the first one's slot
+// instead of sharing its queue words and partial rows
+static hipEvent_t g_slot_ev[64][QSLOTS];
+static bool g_slot_ev_set[64][QSLOTS];
+// (slot creation: a device's own lock, so that its allocation and wait never
+// hold up launches on other devices under g_mu)
+static std::mutex g_dev_mu[64];
 // Per-lane kernel: one launch per EV_CHUNK instances; its bailed ids go to a
 // list of EV_BAIL_CAP entries (16 MB) kept per (device, stream): launches of
 // one stream run in order, so they can share it.  Bails are rare
@@ -408,7 +441,30 @@ struct ListUse {
   hipStream_t st;
   bool queued = false;
   ~ListUse() {
-    if (e && queued && hipEventRecord(e->ev, st) == hipSuccess) e->ev_set = true;
+    if (!e || !queued) return;
+    if (hipEventRecord(e->ev, st) == hipSuccess) {
+      e->ev_set = true;
+    } else {
+      // (no event behind these launches: wait for them here, so that a later
+      // owner taking the entry over cannot share the lists with them)
+      (void)hipStreamSynchronize(st);
+      e->ev_set = false;
+    }
+  }
+};
+
+// The same for the chunk's scratch slot (g_slot_ev), on every exit of the chunk
+struct SlotUse {
+  int dev, sidx;
+  hipStream_t st;
+  ~SlotUse() {
+    if (sidx < 0) return;
+    if (hipEventRecord(g_slot_ev[dev][sidx], st) == hipSuccess) {
+      g_slot_ev_set[dev][sidx] = true;
+    } else {
+      (void)hipStreamSynchronize(st);
+      g_slot_ev_set[dev][sidx] = false;
+    }
   }
 };
 
@@ -423,16 +479,84 @@ extern "C" void pxb_stream_release(int dev, void* stream) {
     if (g_lists[dev][k].owned && g_lists[dev][k].s == st) g_lists[dev][k].owned = false;
 }
 
-// per-device scratch of pxb_run_device (callers hold g_mu)
+// per-device scratch of pxb_run_device, created on the current device `dev`
+// (callers do NOT hold g_mu: the allocation and the wait for its zeroing take
+// only this device's lock, so a device's first launch holds up no launch on
+// another device); published under g_mu
 static int ensure_slots(int dev) {
-  if (g_slots[dev]) return PXB_OK;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_slots[dev]) return PXB_OK;
+  }
+  std::lock_guard<std::mutex> dl(g_dev_mu[dev]);
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_slots[dev]) return PXB_OK;            // (another thread made them meanwhile)
+  }
   unsigned long long* q = nullptr;
-  HIPCHK(hipMalloc(&q, (HAND_U64 + 16) * sizeof(unsigned long long)));
-  HIPCHK(hipMemset(q, 0, (HAND_U64 + 16) * sizeof(unsigned long long)));
-  HIPCHK(hipDeviceSynchronize());
+  hipStream_t zs = nullptr;
+  hipError_t e = hipMalloc(&q, (HAND_U64 + 16) * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipStreamCreateWithFlags(&zs, hipStreamNonBlocking);
+  // (the zeroing completes before any launch can use the slots: a private
+  // stream, so this waits for nothing else on the device)
+  if (e == hipSuccess) e = hipMemsetAsync(q, 0, (HAND_U64 + 16) * sizeof(unsigned long long), zs);
+  if (e == hipSuccess) e = hipStreamSynchronize(zs);
+  for (int k = 0; k < QSLOTS && e == hipSuccess; ++k)
+    if (!g_slot_ev[dev][k]) e = hipEventCreateWithFlags(&g_slot_ev[dev][k], hipEventDisableTiming);
+  if (zs) (void)hipStreamDestroy(zs);
+  if (e != hipSuccess) {
+    if (q) (void)hipFree(q);
+    return hip_fail(e);
+  }
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (int k = 0; k < QSLOTS; ++k) g_slot_ev_set[dev][k] = false;
   g_slots[dev] = q;
   return PXB_OK;
 }
+
+static void read_hooks_locked() {
+  Hooks h;
+  memset(&h, 0, sizeof(h));
+  auto flag = [](const char* name) {
+    const char* v = getenv(name);
+    return v && atoi(v) > 0;
+  };
+  auto num = [](const char* name, int dflt) {
+    const char* v = getenv(name);
+    return v ? atoi(v) : dflt;
+  };
+  h.no_ev = flag("PXB_NO_EV");
+  h.no_ff1 = flag("PXB_NO_FF1");
+  h.no_ffp = flag("PXB_NO_FFP");
+  h.no_split = flag("PXB_NO_SPLIT");
+  h.no_tight = flag("PXB_NO_TIGHT");
+  h.fail_after_first = flag("PXB_FAIL_AFTER_FIRST");
+  h.ff1_bail = flag("PXB_FF1_BAIL");
+  h.bail_cap = num("PXB_EV_BAIL_CAP", -1);
+  h.blocks_per_cu = std::max(0, num("PXB_BLOCKS_PER_CU", 0));
+  const int fo = num("PXB_FF1_OVERSUB", 0), po = num("PXB_FFP_OVERSUB", 0);
+  h.ff1_oversub = (fo > 0 && fo <= 64) ? fo : 0;
+  h.ffp_oversub = (po > 0 && po <= 64) ? po : 0;
+  const char* ph = getenv("PXB_MULTI_FAIL_PHASE");
+  if (ph) snprintf(h.multi_fail_phase, sizeof(h.multi_fail_phase), "%s", ph);
+  h.multi_fail_device = num("PXB_MULTI_FAIL_DEVICE", -1);
+  g_hooks = h;
+  g_hooks_read = true;
+}
+
+// the hooks in force (a copy: callers read it without the lock)
+static Hooks hooks() {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_hooks_read) read_hooks_locked();
+  return g_hooks;
+}
+
+// (paxos_multi.cpp's failure injection: device g fails in `phase`)
+bool multi_fail_injected(const char* phase, int g) {
+  const Hooks h = hooks();
+  return h.multi_fail_phase[0] && strcmp(h.multi_fail_phase, phase) == 0 && h.multi_fail_device == g;
+}
+
 
 extern "C" void pxb_multi_release(void);   // paxos_multi.cpp
 extern "C" void pxb_wire_release(void);    // paxos_wire.hip
@@ -444,21 +568,25 @@ int pxb_init(int n_devices) {
   if (G > visible || G > 64) return PXB_E_INVAL;
   int cur = 0;
   HIPCHK(hipGetDevice(&cur));
-  std::lock_guard<std::mutex> lk(g_mu);
+  (void)hooks();                       // (the test hooks: read now, not in a launch)
   for (int d = 0; d < G; ++d) {
     HIPCHK(hipSetDevice(d));
     if (int rc = ensure_slots(d)) {
       (void)hipSetDevice(cur);
       return rc;
     }
-    if (!g_cus[d]) {
-      hipDeviceProp_t prop;
-      HIPCHK(hipGetDeviceProperties(&prop, d));
-      g_cus[d] = prop.multiProcessorCount;
-    }
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, d));
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_cus[d]) g_cus[d] = prop.multiProcessorCount;
   }
   HIPCHK(hipSetDevice(cur));
   return PXB_OK;
+}
+
+void pxb_reload_hooks(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  read_hooks_locked();
 }
 
 int pxb_shutdown(void) {
@@ -473,6 +601,11 @@ int pxb_shutdown(void) {
       if (hipSetDevice(d) != hipSuccess || hipDeviceSynchronize() != hipSuccess) rc = PXB_E_HIP;
       if (g_slots[d]) (void)hipFree(g_slots[d]);
       g_slots[d] = nullptr;
+      for (int k = 0; k < QSLOTS; ++k) {
+        if (g_slot_ev[d][k]) (void)hipEventDestroy(g_slot_ev[d][k]);
+        g_slot_ev[d][k] = nullptr;
+        g_slot_ev_set[d][k] = false;
+      }
       for (int k = 0; k < g_nlists[d]; ++k) {
         if (g_lists[d][k].bail) (void)hipFree(g_lists[d][k].bail);
         if (g_lists[d][k].split) (void)hipFree(g_lists[d][k].split);
@@ -515,12 +648,19 @@ int pxb_handoff_counts(int dev, uint64_t* out2, int reset) {
     out2[0] = out2[1] = 0;
     return PXB_OK;
   }
+  // (one reader at a time: the exchange's two output words are shared)
+  static std::mutex hand_mu;
+  std::lock_guard<std::mutex> hl(hand_mu);
   int cur = 0;
   HIPCHK(hipGetDevice(&cur));
   HIPCHK(hipSetDevice(dev));
   hipError_t e = hipDeviceSynchronize();
-  if (e == hipSuccess) e = hipMemcpy(out2, h, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost);
-  if (e == hipSuccess && reset) e = hipMemset(h, 0, 2 * sizeof(uint64_t));
+  if (e == hipSuccess) {
+    // read and (reset) zero in one atomic per count, on the device
+    hipLaunchKernelGGL(hand_xchg_kernel, dim3(1), dim3(64), 0, nullptr, h, h + 2, reset ? 1 : 0);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipMemcpy(out2, h + 2, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost);
   (void)hipSetDevice(cur);
   return e == hipSuccess ? PXB_OK : hip_fail(e);
 }
@@ -534,6 +674,7 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
   int dev = 0;
   HIPCHK(hipGetDevice(&dev));
   if (dev < 0 || dev >= 64) return PXB_E_NODEV;
+  const Hooks hk = hooks();
   const bool logm = cfg->n_ticks > 1;   // log mode: several Ticks per proposer
   // fault-free schedule: no message is lost, delayed past the next step or sent
   // to an isolated acceptor (Tick skew is allowed)
@@ -545,23 +686,18 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
   // (MI355X, 2^22 instances, ms: config 5 148 vs 247; P = 3, N = 9 with delays
   // to 12: 347 vs 689; P = 2, N = 9, delays to 12: 97 vs 247).
   // PXB_NO_EV=1 forces the general kernel.
-  const char* no_ev = getenv("PXB_NO_EV");
   // (faulty log mode too: the per-lane kernel's log-mode fields, 8-step wheel)
-  bool use_ev = !ff && ev::eligible(cfg) && !(no_ev && atoi(no_ev) > 0);
+  bool use_ev = !ff && ev::eligible(cfg) && !hk.no_ev;
   // tests: a smaller bailed-id list, to exercise its overflow path
-  const char* cap_s = getenv("PXB_EV_BAIL_CAP");
-  const uint32_t bail_cap = (cap_s && atoi(cap_s) >= 0) ? std::min<uint32_t>((uint32_t)atoi(cap_s), EV_BAIL_CAP)
-                                                      : EV_BAIL_CAP;
+  const uint32_t bail_cap = hk.bail_cap >= 0 ? std::min<uint32_t>((uint32_t)hk.bail_cap, EV_BAIL_CAP) : EV_BAIL_CAP;
   // fault-free single-proposer batches (configs 1, 2) run one instance per
   // lane on paxos_ff1_kernel, its (never expected) bails on the general
   // faulty kernel; PXB_NO_FF1=1 keeps them on the general fault-free kernel
-  const char* no_ff1 = getenv("PXB_NO_FF1");
-  const bool use_ff1 = ff && !logm && cfg->n_proposers == 1 && !(no_ff1 && atoi(no_ff1) > 0);
+  const bool use_ff1 = ff && !logm && cfg->n_proposers == 1 && !hk.no_ff1;
   // the other fault-free batches (duelling proposers, log mode) on
   // paxos_ffp_kernel, its bails on the general faulty kernel; PXB_NO_FFP=1
   // keeps them on the general fault-free kernel
-  const char* no_ffp = getenv("PXB_NO_FFP");
-  const bool use_ffp = ff && !use_ff1 && !(no_ffp && atoi(no_ffp) > 0);
+  const bool use_ffp = ff && !use_ff1 && !hk.no_ffp;
   kernel_fn fn = pick(cfg->n_proposers, cfg->n_acceptors, logm, ff && !use_ff1 && !use_ffp);
   if (!fn) return PXB_E_INVAL;
   const ff1_kernel_ptr ffn = use_ff1 ? ff1_pick(cfg->n_acceptors) : nullptr;
@@ -578,26 +714,29 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
   // general kernel.  PXB_NO_SPLIT=1 turns it off.
   // tests only: PXB_FAIL_AFTER_FIRST=1 fails every chunk right after its first
   // per-lane launch (the list and slot bookkeeping of the failure path)
-  const char* faf = getenv("PXB_FAIL_AFTER_FIRST");
-  const bool fail_after_first = faf && atoi(faf) > 0;
-  const char* no_split = getenv("PXB_NO_SPLIT");
-  const bool may_split = use_ev && (cfg->flags & PXB_CFG_RANDOMIZE) && cfg->n_proposers == 3 &&
-                         !(no_split && atoi(no_split) > 0);
+  const bool fail_after_first = hk.fail_after_first;
+  const bool may_split = use_ev && (cfg->flags & PXB_CFG_RANDOMIZE) && cfg->n_proposers == 3 && !hk.no_split;
   // Tight routing of two-proposer simple schedules whose layout-6 lane takes
   // more than 52 LDS words (config 4: 60 words, 10 waves per CU, so half the
   // SIMDs run 2 waves and half 3): layout 7 (52 words, 12 waves per CU)
   // runs over the chunk first and lists its bails (config 4: 0.5 %, nearly all
   // a full 3-deep response FIFO) for layout 6 over that list, whose own bails
   // go to the general kernel.  PXB_NO_TIGHT=1 turns it off.
-  const char* no_tight = getenv("PXB_NO_TIGHT");
-  const bool may_tight = use_ev && layout == 6 && cfg->n_proposers == 2 && cfg->n_proposers * cfg->n_acceptors > 10 &&
-                         !(no_tight && atoi(no_tight) > 0);
+  // Only where its hand-off rate is measured small: N = 6, 7 (host model,
+  // tools/wave_model.cpp NACC=6/7/8 TIGHT=1 on config 4's schedule: 0.11 %,
+  // 0.76 %, 2.8 %; at N = 8 the tight lane has 53 words, so it would not reach
+  // 12 waves per CU anyway, and its 21-word pool serves 16 response links).
+  // A list that overflowed (above a quarter of the chunk) would have the
+  // general kernel re-run the whole chunk: exact, but slow.
+  const bool may_tight = use_ev && layout == 6 && cfg->n_proposers == 2 && cfg->n_acceptors >= 6 &&
+                         cfg->n_acceptors <= 7 && !hk.no_tight;
   const ev_kernel_ptr sfn = may_split ? ev_pick(2, cfg->n_acceptors, layout)
                             : may_tight ? ev_pick(2, cfg->n_acceptors, 7) : nullptr;
   // (split: the two-stage routing of either kind)
   bool split = false;
   const hipStream_t st = (hipStream_t)stream;
   int occ, cus, eocc = 0, socc = 0;
+  if (int rc2 = ensure_slots(dev)) return rc2;   // (not under g_mu: see ensure_slots)
   {
     std::lock_guard<std::mutex> lk(g_mu);
     if (!g_cus[dev]) {
@@ -652,12 +791,10 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
         split = socc > eocc;
       }
     }
-    if (int rc2 = ensure_slots(dev)) return rc2;
-    const char* cap_env = getenv("PXB_BLOCKS_PER_CU");   // tests / experiments: cap residency
-    if (cap_env && atoi(cap_env) > 0) {
-      occ = std::min(occ, atoi(cap_env));
-      if (eocc) eocc = std::min(eocc, atoi(cap_env));
-      if (socc) socc = std::min(socc, atoi(cap_env));
+    if (hk.blocks_per_cu > 0) {                 // tests / experiments: cap residency
+      occ = std::min(occ, hk.blocks_per_cu);
+      if (eocc) eocc = std::min(eocc, hk.blocks_per_cu);
+      if (socc) socc = std::min(socc, hk.blocks_per_cu);
     }
   }
   KParams kp;
@@ -722,15 +859,17 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
     EvLists* lent = nullptr;
     // (held until this chunk's launches are enqueued: see EvLists)
     std::unique_lock<std::mutex> lk(g_mu);
-    {
-      const int sidx = (int)(g_qseq[dev]++ % QSLOTS);
-      slot = g_slots[dev] + (size_t)sidx * SLOT_U64;
-      kp.part = slot;
-      kp.queue = reinterpret_cast<uint32_t*>(slot + 2 * ROWS_U64);
-      if (use_ev || use_ff1 || use_ffp)
-        if (int rc2 = stream_lists(dev, st, split, &bail, &slist, &lent)) return rc2;
-    }
-    // the lists' event goes behind whatever this chunk queues, on every exit
+    const int sidx = (int)(g_qseq[dev]++ % QSLOTS);
+    slot = g_slots[dev] + (size_t)sidx * SLOT_U64;
+    kp.part = slot;
+    kp.queue = reinterpret_cast<uint32_t*>(slot + 2 * ROWS_U64);
+    // after the slot's last user (another stream's chunk may still run on it)
+    if (g_slot_ev_set[dev][sidx]) HIPCHK(hipStreamWaitEvent(st, g_slot_ev[dev][sidx], 0));
+    // the slot's event goes behind whatever this chunk queues, on every exit
+    SlotUse suse{dev, sidx, st};
+    if (use_ev || use_ff1 || use_ffp)
+      if (int rc2 = stream_lists(dev, st, split, &bail, &slist, &lent)) return rc2;
+    // the lists' event likewise
     ListUse use{lent, st, lent != nullptr};
     // a launch that fails after an earlier one of this chunk has queued leaves
     // the slot half used: zero it behind the queued work before reporting
@@ -756,11 +895,9 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
       fp.bail_ids = bail;
       fp.bail_n = kp.queue + Q_BAIL;
       fp.bail_cap = bail_cap;
-      const char* fb = getenv("PXB_FF1_BAIL");           // tests: hand every instance to the general kernel
-      fp.bail_all = (fb && atoi(fb) > 0) ? 1u : 0u;
+      fp.bail_all = hk.ff1_bail ? 1u : 0u;               // tests: hand every instance to the general kernel
       // FF1_OVERSUB x the resident blocks (PXB_FF1_OVERSUB=k: k, A/B)
-      const char* fos = getenv("PXB_FF1_OVERSUB");
-      const uint64_t over = (fos && atoi(fos) > 0 && atoi(fos) <= 64) ? (uint64_t)atoi(fos) : FF1_OVERSUB;
+      const uint64_t over = hk.ff1_oversub ? (uint64_t)hk.ff1_oversub : FF1_OVERSUB;
       const uint64_t fres = (uint64_t)eocc * (uint64_t)cus * over;
       const unsigned fgrid = (unsigned)std::min<uint64_t>((nc + 255) / 256, fres);
       hipLaunchKernelGGL(ffn, dim3(fgrid), dim3(256), 0, st, fp);
@@ -791,10 +928,8 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
       fp.bail_ids = bail;
       fp.bail_n = kp.queue + Q_BAIL;
       fp.bail_cap = bail_cap;
-      const char* fb = getenv("PXB_FF1_BAIL");           // tests: hand every instance to the general kernel
-      fp.bail_all = (fb && atoi(fb) > 0) ? 1u : 0u;
-      const char* fos = getenv("PXB_FFP_OVERSUB");    // (A/B)
-      const uint64_t over = (fos && atoi(fos) > 0 && atoi(fos) <= 64) ? (uint64_t)atoi(fos) : FF1_OVERSUB;
+      fp.bail_all = hk.ff1_bail ? 1u : 0u;               // tests: hand every instance to the general kernel
+      const uint64_t over = hk.ffp_oversub ? (uint64_t)hk.ffp_oversub : FF1_OVERSUB;   // (A/B)
       const uint64_t fres = (uint64_t)eocc * (uint64_t)cus * over;
       const unsigned fgrid = (unsigned)std::min<uint64_t>((nc + 255) / 256, fres);
       hipLaunchKernelGGL(pfn, dim3(fgrid), dim3(256), 0, st, fp);

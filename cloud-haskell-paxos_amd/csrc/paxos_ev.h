@@ -274,6 +274,7 @@ template <int PM, int N, int POOL, int W, bool CMP, class Mem, bool EARLY = true
           int SP = 0>
 struct EvLane {
   using S = Shape<PM, N, POOL, W, CMP, LG, SL, SP>;
+  static constexpr bool kEarly = EARLY;
   // acceptor fields (Layouts): dead bit, log-length shift (LG: in accv) and its limit
   static constexpr uint32_t A_DEAD = LG ? 24 : 26, A_LEN = LG ? 14 : 27, A_LEN_MAX = LG ? (1u << 18) - 1u : 31;
   using pool_mask_t = typename std::conditional<(POOL > 32), unsigned long long, uint32_t>::type;

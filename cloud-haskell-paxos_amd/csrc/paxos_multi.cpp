@@ -19,6 +19,8 @@
 #include "../../include/paxos_batch.h"
 #include "shard_runner.h"
 
+extern "C" bool multi_fail_injected(const char* phase, int g);   // paxos_batch.hip
+
 namespace {
 
 std::mutex g_comm_mu;
@@ -78,11 +80,8 @@ void abort_comms() {
 
 // tests: make device `g` fail in a phase ("setup" / "compute"), to check that
 // the call returns the error promptly instead of hanging in the collective
-bool injected(const char* phase, int g) {
-  const char* p = getenv("PXB_MULTI_FAIL_PHASE");
-  const char* d = getenv("PXB_MULTI_FAIL_DEVICE");
-  return p && d && strcmp(p, phase) == 0 && atoi(d) == g;
-}
+// (PXB_MULTI_FAIL_PHASE / _DEVICE, read with the library's other test hooks)
+bool injected(const char* phase, int g) { return multi_fail_injected(phase, g); }
 
 
 struct HipShards {

@@ -11,8 +11,11 @@
 namespace pxb {
 namespace ev {
 
-template <int PM, int N, int POOL, int W, class Mem, bool EARLY>
-__device__ void trace_record(const EvLane<PM, N, POOL, W, false, Mem, EARLY>& L, uint32_t step, pxb_trace_step* r) {
+template <class Lane>
+__device__ void trace_record(const Lane& L, uint32_t step, pxb_trace_step* r) {
+  constexpr int PM = Lane::S::PM, N = Lane::S::N;
+  constexpr bool LG = Lane::S::LG;
+  constexpr bool EARLY = Lane::kEarly;
   r->step = step;
   // (production variant: copies of a broadcast still to send are not on the
   // links yet, so the count is not the oracle's end-of-step one)
@@ -31,15 +34,24 @@ __device__ void trace_record(const EvLane<PM, N, POOL, W, false, Mem, EARLY>& L,
   for (int p = 0; p < PXB_MAX_PROPOSERS; ++p) {
     pxb_trace_prop q = {0, 0, 0, 0, 0, 0, 0, 0};
     if (p < PM && (uint32_t)p < L.P) {
-      const uint32_t code = 1u;   // every command is c<id>.1 (docs/SEMANTICS.md §2)
       q.ticket = (int32_t)L.p_ticket(p);
-      q.cmd = L.p_cmd(p) ? ((L.p_cmd(p) << 24) | code) : 0u;
       q.acks = L.p_acks(p);
       q.state = L.p_state(p);
       q.mr_t = (int32_t)L.p_mr_t(p);
-      q.mr_v = L.p_mr_v(p) ? ((L.p_mr_v(p) << 24) | code) : 0u;
-      q.r2_v = L.p_r2_v(p) ? ((L.p_r2_v(p) << 24) | code) : 0u;
       q.pending = L.p_pending(p);
+      if constexpr (LG) {
+        // log mode: 14-bit commands id [13:12] | t [11:0] (mr_v | r2_v << 14 in
+        // pw1), the proposer's own command c<p+1>.<t> with t in pw2 (0: Nothing)
+        const uint32_t mv = L.pw1[p] & 0x3FFFu, rv = (L.pw1[p] >> 14) & 0x3FFFu, ct = L.pw2[p];
+        q.cmd = ct ? (((uint32_t)p + 1u) << 24) | ct : 0u;
+        q.mr_v = mv ? Lane::code_of(mv) : 0u;
+        q.r2_v = rv ? Lane::code_of(rv) : 0u;
+      } else {
+        const uint32_t code = 1u;   // every command is c<id>.1 (docs/SEMANTICS.md §2)
+        q.cmd = L.p_cmd(p) ? ((L.p_cmd(p) << 24) | code) : 0u;
+        q.mr_v = L.p_mr_v(p) ? ((L.p_mr_v(p) << 24) | code) : 0u;
+        q.r2_v = L.p_r2_v(p) ? ((L.p_r2_v(p) << 24) | code) : 0u;
+      }
     }
     r->prop[p] = q;
   }
@@ -51,14 +63,16 @@ __device__ void trace_record(const EvLane<PM, N, POOL, W, false, Mem, EARLY>& L,
 // state exactly; EARLY = true (PXB_CFG_TRACE_PRODUCTION): the carry-over
 // variant the batch kernels run (paxos_ev.h, end_op), recorded on entering the
 // next step.
-template <int PM, int N, int W, bool EARLY>
+// LG: log mode (several Ticks per proposer, logs of commands c<id>.<t>): the
+// batch kernels' log-mode shape (layout 4, EvLane<..., LG = true>, 8-step wheel)
+template <int PM, int N, int W, bool EARLY, bool LG = false>
 __global__ __launch_bounds__(64) void paxos_trace_kernel(EvParams p, uint32_t gid, pxb_trace_step* out, uint32_t max,
                                                          uint32_t* status, uint4* res) {
-  constexpr int POOL = EvPool<PM, N, false>::value;
-  using S = Shape<PM, N, POOL, W, false>;
+  constexpr int POOL = EvPool<PM, N, false, LG>::value;
+  using S = Shape<PM, N, POOL, W, false, LG>;
   __shared__ uint32_t lds[S::WORDS * 64];
   if (threadIdx.x != 0) return;
-  EvLane<PM, N, POOL, W, false, LdsMem, EARLY> L;
+  EvLane<PM, N, POOL, W, false, LdsMem, EARLY, LG> L;
   L.m = LdsMem{lds, 0u};
   L.set_keys(p);
   L.init(p, gid);
@@ -93,30 +107,34 @@ __global__ __launch_bounds__(64) void paxos_trace_kernel(EvParams p, uint32_t gi
 
 typedef void (*trace_ptr)(EvParams, uint32_t, pxb_trace_step*, uint32_t, uint32_t*, uint4*);
 
-template <int PM, int W, bool E>
+template <int PM, int W, bool E, bool LG = false>
 static trace_ptr pick_n(uint32_t n) {
   switch (n) {
-    case 2: return paxos_trace_kernel<PM, 2, W, E>;
-    case 3: return paxos_trace_kernel<PM, 3, W, E>;
-    case 4: return paxos_trace_kernel<PM, 4, W, E>;
-    case 5: return paxos_trace_kernel<PM, 5, W, E>;
-    case 6: return paxos_trace_kernel<PM, 6, W, E>;
-    case 7: return paxos_trace_kernel<PM, 7, W, E>;
-    case 8: return paxos_trace_kernel<PM, 8, W, E>;
-    case 9: return paxos_trace_kernel<PM, 9, W, E>;
+    case 2: return paxos_trace_kernel<PM, 2, W, E, LG>;
+    case 3: return paxos_trace_kernel<PM, 3, W, E, LG>;
+    case 4: return paxos_trace_kernel<PM, 4, W, E, LG>;
+    case 5: return paxos_trace_kernel<PM, 5, W, E, LG>;
+    case 6: return paxos_trace_kernel<PM, 6, W, E, LG>;
+    case 7: return paxos_trace_kernel<PM, 7, W, E, LG>;
+    case 8: return paxos_trace_kernel<PM, 8, W, E, LG>;
+    case 9: return paxos_trace_kernel<PM, 9, W, E, LG>;
   }
   return nullptr;
 }
 
+// (log mode: the 8-step wheel only, as the batch kernels' LG shape)
 template <bool E>
-static trace_ptr pick(uint32_t pm, uint32_t n, int w) {
-  switch (pm * 100 + (uint32_t)w) {
-    case 108: return pick_n<1, 8, E>(n);
-    case 116: return pick_n<1, 16, E>(n);
-    case 208: return pick_n<2, 8, E>(n);
-    case 216: return pick_n<2, 16, E>(n);
-    case 308: return pick_n<3, 8, E>(n);
-    case 316: return pick_n<3, 16, E>(n);
+static trace_ptr pick(uint32_t pm, uint32_t n, int w, bool lg) {
+  switch (pm * 1000 + (lg ? 500u : 0u) + (uint32_t)w) {
+    case 1008: return pick_n<1, 8, E>(n);
+    case 1016: return pick_n<1, 16, E>(n);
+    case 2008: return pick_n<2, 8, E>(n);
+    case 2016: return pick_n<2, 16, E>(n);
+    case 3008: return pick_n<3, 8, E>(n);
+    case 3016: return pick_n<3, 16, E>(n);
+    case 1508: return pick_n<1, 8, E, true>(n);
+    case 2508: return pick_n<2, 8, E, true>(n);
+    case 3508: return pick_n<3, 8, E, true>(n);
   }
   return nullptr;
 }
@@ -132,15 +150,17 @@ extern "C" int pxb_trace_instance(const pxb_config* cfg, uint64_t instance, pxb_
       cfg->n_acceptors > PXB_MAX_ACCEPTORS || cfg->delay_max < 1 || cfg->delay_max > PXB_MAX_DELAY ||
       cfg->step_cap < 1 || !eligible(cfg))
     return PXB_E_INVAL;
-  // single decree only: the trace kernel runs the single-decree fields (one
-  // Tick per proposer, 2-bit commands); eligible() admits log mode for the
-  // batch kernels' LG shape, so log mode is refused here explicitly
-  if (cfg->n_ticks > 1) return PXB_E_INVAL;
+  // log mode (n_ticks > 1, ABI 5): the batch kernels' log-mode shape (its
+  // ticker, 14-bit commands, Execute-driven logs); eligible() holds its delays
+  // to the 8-step wheel
+  if (cfg->n_ticks > PXB_MAX_TICKS || (cfg->n_ticks > 1 && (cfg->tick_period < 1 || cfg->tick_period > PXB_MAX_STEP_CAP)))
+    return PXB_E_INVAL;
+  const bool lg = cfg->n_ticks > 1;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return PXB_E_NODEV;
   const bool prod = (cfg->flags & PXB_CFG_TRACE_PRODUCTION) != 0u;
-  const trace_ptr fn = prod ? pick<true>(cfg->n_proposers, cfg->n_acceptors, wheel_for(cfg->delay_max))
-                            : pick<false>(cfg->n_proposers, cfg->n_acceptors, wheel_for(cfg->delay_max));
+  const trace_ptr fn = prod ? pick<true>(cfg->n_proposers, cfg->n_acceptors, wheel_for(cfg->delay_max), lg)
+                            : pick<false>(cfg->n_proposers, cfg->n_acceptors, wheel_for(cfg->delay_max), lg);
   if (!fn) return PXB_E_INVAL;
   EvParams p = make_params(cfg);
   p.first_instance = instance;

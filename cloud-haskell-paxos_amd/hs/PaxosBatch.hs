@@ -144,7 +144,7 @@ foreign import ccall safe "pxb_handoff_counts"
 
 -- | The ABI this module was written against (include/paxos_batch.h).
 expectedAbi :: Int
-expectedAbi = 4
+expectedAbi = 5
 
 -- | pxb_abi_version of the loaded library.
 abiVersion :: IO Int

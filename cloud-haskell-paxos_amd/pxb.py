@@ -166,7 +166,7 @@ def canonical_bytes_nofault(n_acceptors: int) -> int:
 
 # ---- library loading --------------------------------------------------------
 _lib = None
-ABI_VERSION = 4          # PXB_ABI_VERSION of include/paxos_batch.h this mirror binds
+ABI_VERSION = 5          # PXB_ABI_VERSION of include/paxos_batch.h this mirror binds
 
 
 class PaxosError(RuntimeError):
@@ -212,6 +212,8 @@ def load(path: str = LIB_PATH):
     lib.pxb_stream_release.restype = None
     lib.pxb_handoff_counts.argtypes = [C.c_int, vp, C.c_int]
     lib.pxb_handoff_counts.restype = C.c_int
+    lib.pxb_reload_hooks.argtypes = []
+    lib.pxb_reload_hooks.restype = None
     if lib.pxb_abi_version() != ABI_VERSION:          # (a stale build: its struct layouts may differ)
         raise PaxosError("libpaxos_batch.so has ABI %d, this binding expects %d — rebuild it"
                          % (lib.pxb_abi_version(), ABI_VERSION))
@@ -427,6 +429,40 @@ def handoff_counts(dev: int = 0, reset: bool = True):
     out = (C.c_uint64 * 2)()
     check(load().pxb_handoff_counts(dev, C.cast(out, C.c_void_p), 1 if reset else 0))
     return int(out[0]), int(out[1])
+
+
+def reload_hooks():
+    """pxb_reload_hooks: re-read the library's test / A-B hooks (PXB_NO_EV,
+    PXB_NO_TIGHT, PXB_EV_BAIL_CAP, ...) from the environment."""
+    load().pxb_reload_hooks()
+
+
+class hooks:
+    """Context manager for tests and A/B runs: sets the given PXB_* hooks in
+    the environment, has the library re-read them, and restores both on exit.
+
+        with pxb.hooks(PXB_NO_EV="1"):
+            pxb.run(cfg, 0, n)
+    """
+
+    def __init__(self, **env):
+        self.env = {k: str(v) for k, v in env.items()}
+        self.old = {}
+
+    def __enter__(self):
+        self.old = {k: os.environ.get(k) for k in self.env}
+        os.environ.update(self.env)
+        reload_hooks()
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+        reload_hooks()
+        return False
 
 
 def shutdown():

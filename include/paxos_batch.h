@@ -26,8 +26,9 @@
 extern "C" {
 #endif
 
-#define PXB_ABI_VERSION 4   /* 3: pxb_init / pxb_shutdown, n_bytes bound on wire decode;
-                               4: pxb_stream_release, pxb_handoff_counts */
+#define PXB_ABI_VERSION 5   /* 3: pxb_init / pxb_shutdown, n_bytes bound on wire decode;
+                               4: pxb_stream_release, pxb_handoff_counts;
+                               5: pxb_reload_hooks, pxb_trace_instance in log mode */
 
 /* ---- error codes ---------------------------------------------------------- */
 #define PXB_OK          0
@@ -161,10 +162,12 @@ int pxb_run(const pxb_config* cfg, pxb_result* out, uint32_t* log_digest,
  *     log-mode shape, then the general log-mode kernel over its bailed
  *     instances (chunks of 2^26; longer delays: the general log-mode kernel).
  * Each chunk
- * uses one of 64 per-device scratch slots round-robin: at most 64 chunks per
- * device may be in flight at once across streams.  A launch failure after a
- * chunk's first kernel zeroes its slot (behind the queued work) before the
- * error is returned.                                                         */
+ * uses one of 64 per-device scratch slots round-robin; a chunk that takes a
+ * slot makes its stream wait (on the device, hipStreamWaitEvent) for the
+ * event recorded behind the slot's previous chunk, so any number of chunks
+ * may be in flight across streams (a 65th waits for the first's slot).  A
+ * launch failure after a chunk's first kernel zeroes its slot (behind the
+ * queued work) before the error is returned.                                 */
 int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_digest,
                    pxb_acceptor_rec* d_acc, int64_t* d_totals, void* stream);
 
@@ -226,13 +229,16 @@ void pxb_stream_release(int dev, void* stream);
  * (acceptor and proposer states are the end-of-step ones; in_flight is
  * PXB_TRACE_IN_FLIGHT_UNKNOWN while copies are still to send, and a carried
  * step may be recorded although nothing else falls due in it).
- * PXB_E_INVAL for log mode, for
- * step_cap > 4095, or if the instance outgrows the state machine's link
- * capacities (its FIFOs hold 4 messages; the batch kernels then hand it to
- * the general kernel) or max_records.                                        */
+ * Log mode (n_ticks > 1, ABI 5) runs the batch kernels' log-mode shape: the
+ * ticker, Execute-driven logs (the acceptor records' log lengths and digests
+ * per step) and commands c<id>.<t> in the proposer fields.
+ * PXB_E_INVAL for step_cap > 4095, for log mode with delays above 8, or if the
+ * instance outgrows the state machine's link capacities (its FIFOs hold 4
+ * messages; the batch kernels then hand it to the general kernel) or
+ * max_records.                                                               */
 typedef struct pxb_trace_prop {
   int32_t  ticket;           /* _ticket                      Client.hs:60    */
-  uint32_t cmd;              /* _mCommand, (id << 24) | 1 or 0               */
+  uint32_t cmd;              /* _mCommand, (id << 24) | t or 0 (t = 1 single decree) */
   uint32_t acks;             /* _numAcks                                     */
   uint32_t state;            /* 0 Idle, 1 Round1, 2 Round2                    */
   int32_t  mr_t;             /* Round1: MostRecent (ticket, command)          */
@@ -350,6 +356,13 @@ int pxb_wire_decode_host(const uint8_t* in, uint64_t n_bytes, const uint64_t* of
  * device; reset != 0 zeroes the counts after reading.  Observability only:
  * results never depend on it.                                                */
 int pxb_handoff_counts(int dev, uint64_t* out2, int reset);
+
+/* pxb_reload_hooks (ABI 5): re-reads the library's test / A-B hooks from the
+ * environment (PXB_NO_EV, PXB_NO_TIGHT, PXB_EV_BAIL_CAP, PXB_BLOCKS_PER_CU, ...:
+ * routing and capacity switches the GPU tests use).  They are read once, on
+ * pxb_init or the first launch, and then only by this call: the launch path
+ * never calls getenv.  Not for production use; unset, nothing changes.       */
+void pxb_reload_hooks(void);
 
 /* ---- misc ----------------------------------------------------------------- */
 const char* pxb_strerror(int code);

@@ -23,7 +23,7 @@ def test_header_declares_the_boundary():
     names = _declared()
     for f in ("pxb_run", "pxb_run_device", "pxb_acceptor_handle", "pxb_proposer_handle",
               "pxb_strerror", "pxb_last_hip_error", "pxb_abi_version", "pxb_init", "pxb_shutdown",
-              "pxb_run_multi", "pxb_stream_release", "pxb_handoff_counts"):
+              "pxb_run_multi", "pxb_stream_release", "pxb_handoff_counts", "pxb_reload_hooks"):
         assert f in names
 
 
@@ -60,9 +60,14 @@ int main(void) {
 
 def test_misc_entry_points_without_gpu():
     lib = pxb.load()
-    assert lib.pxb_abi_version() == 4            # 4: pxb_stream_release, pxb_handoff_counts
-    assert "#define PXB_ABI_VERSION 4" in open(HEADER).read()
-    assert pxb.ABI_VERSION == 4
+    assert lib.pxb_abi_version() == 5            # 5: pxb_reload_hooks, log-mode traces
+    assert "#define PXB_ABI_VERSION 5" in open(HEADER).read()
+    assert pxb.ABI_VERSION == 5
+    # the test hooks are re-read on request (no GPU call), and restored
+    import os
+    with pxb.hooks(PXB_NO_EV="1", PXB_EV_BAIL_CAP="3"):
+        assert os.environ["PXB_NO_EV"] == "1"
+    assert "PXB_NO_EV" not in os.environ and "PXB_EV_BAIL_CAP" not in os.environ
     # no scratch on a device yet (no GPU here): zero counts, no HIP call
     out = (C.c_uint64 * 2)(7, 7)
     assert lib.pxb_handoff_counts(0, C.cast(out, C.c_void_p), 0) == 0 and list(out) == [0, 0]
@@ -81,21 +86,28 @@ def test_invalid_config_rejected():
     assert lib.pxb_run_device(C.byref(bad), None, None, None, C.cast(tot, C.c_void_p), None) == pxb.PXB_E_INVAL
 
 
-def test_trace_refuses_log_mode():
-    """pxb_trace_instance runs the single-decree fields only: a log-mode config
-    (n_ticks > 1, which the batch kernels' LG shape admits) is PXB_E_INVAL,
-    checked before any device call (so on every host, GPU or not)."""
+def test_trace_log_mode_validation():
+    """pxb_trace_instance runs log mode (ABI 5) on the batch kernels' LG shape:
+    a log-mode config passes validation (PXB_E_NODEV without a GPU, OK with
+    one); delays above the LG shape's 8-step wheel, or a tick period of 0, are
+    PXB_E_INVAL, checked before any device call (so on every host)."""
+    import dataclasses
     import numpy as np
     lib = pxb.load()
     buf = np.zeros((16, pxb.TRACE_WORDS), dtype=np.uint32)
     n = C.c_uint32(0)
     res = np.zeros(4, dtype=np.uint32)
-    for cfg in (pxb.LOG_CONFIG, pxb.LOG_FAULTY_CONFIG):
+
+    def rc(cfg):
         c = cfg.to_c(0, 1)
-        assert lib.pxb_trace_instance(C.byref(c), 0, C.c_void_p(buf.ctypes.data), 16, C.byref(n),
-                                      C.c_void_p(res.ctypes.data)) == pxb.PXB_E_INVAL
-        with pytest.raises(pxb.PaxosError, match="invalid argument"):
-            pxb.trace_instance(cfg, 0, max_records=16)
+        return lib.pxb_trace_instance(C.byref(c), 0, C.c_void_p(buf.ctypes.data), 16, C.byref(n),
+                                      C.c_void_p(res.ctypes.data))
+    for cfg in (pxb.LOG_CONFIG, pxb.LOG_FAULTY_CONFIG):
+        assert rc(cfg) in (pxb.PXB_OK, pxb.PXB_E_NODEV)
+    assert rc(dataclasses.replace(pxb.LOG_FAULTY_CONFIG, delay_max=9)) == pxb.PXB_E_INVAL
+    assert rc(dataclasses.replace(pxb.LOG_FAULTY_CONFIG, tick_period=0)) == pxb.PXB_E_INVAL
+    with pytest.raises(pxb.PaxosError, match="invalid argument"):
+        pxb.trace_instance(dataclasses.replace(pxb.LOG_FAULTY_CONFIG, delay_max=12), 0, max_records=16)
 
 
 def test_no_cpu_fallback_without_gpu():

@@ -250,11 +250,8 @@ def test_per_lane_bail_list_overflow(gpu_lib, cap):
     general kernel; when the list overflows, the general kernel re-runs the
     whole chunk and the per-lane totals are dropped.  Results and totals stay
     exact either way (config 4 bails ~1.4 % of instances)."""
-    os.environ["PXB_EV_BAIL_CAP"] = str(cap)
-    try:
+    with pxb.hooks(PXB_EV_BAIL_CAP=str(cap)):
         _cmp(pxb.CONFIGS[4], 1 << 30, 30000)
-    finally:
-        del os.environ["PXB_EV_BAIL_CAP"]
 
 
 def test_per_lane_matches_general_kernel(gpu_lib):
@@ -262,11 +259,8 @@ def test_per_lane_matches_general_kernel(gpu_lib):
     general kernel (PXB_NO_EV=1) give identical results, digests and totals."""
     cfg = pxb.CONFIGS[4]
     a = pxb.run(cfg, 777, 50000, want_acceptors=True)
-    os.environ["PXB_NO_EV"] = "1"
-    try:
+    with pxb.hooks(PXB_NO_EV="1"):
         b = pxb.run(cfg, 777, 50000, want_acceptors=True)
-    finally:
-        del os.environ["PXB_NO_EV"]
     for x, y in zip(a[:3], b[:3]):
         assert np.array_equal(x, y)
     assert a[3] == b[3]
@@ -282,27 +276,16 @@ def test_config5_split_matches_other_routings(gpu_lib, first):
     cfg = pxb.CONFIGS[5]
     a = pxb.run(cfg, first, 60000, want_acceptors=True)
     for env in ("PXB_NO_SPLIT", "PXB_NO_EV"):
-        os.environ[env] = "1"
-        try:
+        with pxb.hooks(**{env: "1"}):
             b = pxb.run(cfg, first, 60000, want_acceptors=True)
-        finally:
-            del os.environ[env]
         for x, y in zip(a[:3], b[:3]):
             assert np.array_equal(x, y), env
         assert a[3] == b[3], env
 
 
 def _with_env(env, fn):
-    old = {k: os.environ.get(k) for k in env}
-    os.environ.update(env)
-    try:
+    with pxb.hooks(**env):
         return fn()
-    finally:
-        for k, v in old.items():
-            if v is None:
-                del os.environ[k]
-            else:
-                os.environ[k] = v
 
 
 @pytest.mark.parametrize("first", [31337, (1 << 32) - 25000])
@@ -374,11 +357,8 @@ def test_config5_split_list_overflow(gpu_lib, cap):
     """The split routing's id lists overflowing (cap 0: the P = 3 list, so the
     second per-lane kernel runs nothing and marks its own list overflowed;
     5000: either): the general kernel re-runs the chunk; exact either way."""
-    os.environ["PXB_EV_BAIL_CAP"] = str(cap)
-    try:
+    with pxb.hooks(PXB_EV_BAIL_CAP=str(cap)):
         _cmp(pxb.CONFIGS[5], (1 << 32) - 7000, 14000)
-    finally:
-        del os.environ["PXB_EV_BAIL_CAP"]
 
 
 @pytest.mark.parametrize("c", [2, 6])
@@ -402,11 +382,8 @@ def test_ff1_bails_run_on_general_kernel(gpu_lib, c, n):
     (paxos_ff1.h); an instance it hands back runs on the general faulty
     kernel.  PXB_FF1_BAIL=1 hands back every instance: still exact."""
     cfg = pxb.Config(seed=0xFF1, n_proposers=1, n_acceptors=7, skew_max=5) if c == "skew" else pxb.CONFIGS[c]
-    os.environ["PXB_FF1_BAIL"] = "1"
-    try:
+    with pxb.hooks(PXB_FF1_BAIL="1"):
         _cmp(cfg, 123, n)
-    finally:
-        del os.environ["PXB_FF1_BAIL"]
 
 
 @pytest.mark.parametrize("N", [2, 3, 4, 5, 6, 7, 8, 9])
@@ -416,11 +393,8 @@ def test_ff1_matches_general_fault_free_kernel(gpu_lib, N):
     some instances."""
     cfg = pxb.Config(seed=0xF0 + N, n_proposers=1, n_acceptors=N, skew_max=9, step_cap=12)
     a = _cmp(cfg, (1 << 32) - 5000, 10000)
-    os.environ["PXB_NO_FF1"] = "1"
-    try:
+    with pxb.hooks(PXB_NO_FF1="1"):
         b = _cmp(cfg, (1 << 32) - 5000, 10000)
-    finally:
-        del os.environ["PXB_NO_FF1"]
     assert np.array_equal(a[0], b[0]) and a[1] == b[1]
     assert a[1]["step_cap"] > 0 and a[1]["decided"] > 0
 
@@ -437,11 +411,8 @@ def test_ffp_matches_general_fault_free_kernel(gpu_lib, P, N, ticks, period, ske
                      n_ticks=ticks, tick_period=period)
     a = _cmp(cfg, (1 << 32) - 1500, 3000)
     for env in ("PXB_NO_FFP", "PXB_FF1_BAIL"):
-        os.environ[env] = "1"
-        try:
+        with pxb.hooks(**{env: "1"}):
             b = _cmp(cfg, (1 << 32) - 1500, 3000)
-        finally:
-            del os.environ[env]
         assert np.array_equal(a[0], b[0]) and a[1] == b[1], env
 
 
@@ -479,11 +450,8 @@ def test_work_queue_flush_keeps_totals_exact(gpu_lib):
     still equal the per-instance results."""
     cfg = pxb.Config(seed=0xF1, n_proposers=1, n_acceptors=3, delay_max=2, step_cap=64)
     n = 1 << 24
-    os.environ["PXB_BLOCKS_PER_CU"] = "1"
-    try:
+    with pxb.hooks(PXB_BLOCKS_PER_CU="1"):
         res, _, _, cnt = pxb.run(cfg, 5, n, want_digests=False)
-    finally:
-        del os.environ["PXB_BLOCKS_PER_CU"]
     flags = res[:, 3] & 0xFF
     assert cnt["instances"] == n
     assert cnt["decided"] == int((res[:, 0] != 0).sum())
@@ -512,6 +480,70 @@ def test_work_queue_many_launches(gpu_lib):
     eres, _, _, ecnt = oracle_c.run_cpu(cfg, 0, k * n, threads=THREADS)
     assert np.array_equal(out.cpu().numpy().view(np.uint32), eres)
     assert pxb.counters_dict(tot.cpu().tolist()) == ecnt
+
+
+def test_scratch_slots_across_streams_without_sync(gpu_lib):
+    """120 config-4 chunks enqueued round-robin on 3 streams with no host sync
+    in between: far more than the device's 64 scratch slots are in flight at
+    once, so chunk k + 64 takes the slot of chunk k while chunk k may still run
+    on another stream.  Each slot's event (recorded behind its finalize) makes
+    the new user's stream wait for it: results, digests and the per-stream
+    totals equal the oracle's (a shared slot would mix queue words and partial
+    rows of two chunks)."""
+    import torch
+    cfg = pxb.CONFIGS[4]
+    n, k, S = 211, 120, 3
+    streams = [torch.cuda.Stream() for _ in range(S)]
+    out = torch.zeros((k * n, 4), dtype=torch.int32, device="cuda")
+    dig = torch.zeros((k * n, cfg.n_acceptors), dtype=torch.int32, device="cuda")
+    tots = [torch.zeros(16, dtype=torch.int64, device="cuda") for _ in range(S)]
+    torch.cuda.synchronize()
+    for j in range(k):
+        st = streams[j % S]
+        pxb.run_device(cfg, j * n, n, d_results=out[j * n:(j + 1) * n], d_digests=dig[j * n:(j + 1) * n],
+                       d_totals=tots[j % S], stream=st.cuda_stream)
+    torch.cuda.synchronize()
+    eres, edig, _, _ = oracle_c.run_cpu(cfg, 0, k * n, threads=THREADS)
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), eres)
+    assert np.array_equal(dig.cpu().numpy().view(np.uint32), edig)
+    for s in range(S):
+        ids = [j for j in range(k) if j % S == s]
+        want = None
+        for j in ids:
+            _, _, _, c = oracle_c.run_cpu(cfg, j * n, n, threads=THREADS)
+            want = c if want is None else {key: want[key] + c[key] for key in want}
+        assert pxb.counters_dict(tots[s].cpu().tolist()) == want, s
+
+
+@pytest.mark.parametrize("N", [6, 8])
+def test_tight_routing_topologies(gpu_lib, N):
+    """The tight routing (layout 7 first) is taken only where its hand-off rate
+    is measured small: P = 2 with N = 6 or 7 on a simple schedule (host model,
+    tools/wave_model.cpp: N = 6 0.11 %, N = 7 0.76 %, N = 8 2.8 %).  N = 6 runs
+    tight and hands on < 1 %; N = 8 runs layout 6 alone (no second per-lane
+    stage: h2 == 0).  Both exact against the oracle."""
+    cfg = pxb.Config(seed=0x5EED0004 + N, n_proposers=2, n_acceptors=N, delay_max=4, crash_ppm=200000,
+                     crash_len_max=16, crash_start_max=8, step_cap=256)
+    n = 60000
+    pxb.handoff_counts(0, reset=True)
+    _cmp(cfg, 1 << 33, n, want_acc=False)
+    h1, h2 = pxb.handoff_counts(0, reset=True)
+    if N == 6:
+        assert 0 < h1 < n // 100, (h1, h2)
+    else:
+        assert h1 < n // 100 and h2 == 0, (h1, h2)
+
+
+def test_handoff_counts_read_and_reset(gpu_lib):
+    """pxb_handoff_counts reads and zeroes in one device atomic per count: a
+    read without reset keeps the counts, a reset read returns them and leaves
+    zero."""
+    pxb.handoff_counts(0, reset=True)
+    pxb.run(pxb.CONFIGS[4], 1 << 34, 60000, want_results=False, want_digests=False)
+    a = pxb.handoff_counts(0, reset=False)
+    b = pxb.handoff_counts(0, reset=True)
+    c = pxb.handoff_counts(0, reset=True)
+    assert a == b and a[0] > 0 and c == (0, 0)
 
 
 # ---- single-handler hooks: the kernel's device functions vs oracle handlers --
@@ -766,14 +798,11 @@ def test_run_multi_shard_failure_returns_promptly(gpu_lib, phase):
     works."""
     import time
     cfg = pxb.CONFIGS[3]
-    os.environ["PXB_MULTI_FAIL_PHASE"], os.environ["PXB_MULTI_FAIL_DEVICE"] = phase, "0"
-    try:
+    with pxb.hooks(PXB_MULTI_FAIL_PHASE=phase, PXB_MULTI_FAIL_DEVICE="0"):
         t0 = time.perf_counter()
         with pytest.raises(pxb.PaxosError):
             pxb.run_multi(cfg, 0, 5000)
         assert time.perf_counter() - t0 < 60
-    finally:
-        del os.environ["PXB_MULTI_FAIL_PHASE"], os.environ["PXB_MULTI_FAIL_DEVICE"]
     res, _, cnt = pxb.run_multi(cfg, 0, 5000)
     assert cnt["instances"] == 5000
 
@@ -876,7 +905,8 @@ def _as_rec(g):
             "prop": [tuple(int(x) for x in r) for r in g["prop"]]}
 
 
-@pytest.mark.parametrize("c,inst", [(3, 0), (3, 17), (4, 5), (4, 123456), (5, 9), (5, 1000)])
+@pytest.mark.parametrize("c,inst", [(3, 0), (3, 17), (4, 5), (4, 123456), (5, 9), (5, 1000),
+                                    (7, 3), (7, 2024), (7, 77777)])
 def test_trace_matches_oracle_steps(gpu_lib, c, inst):
     """Every step the GPU trace records equals the oracle's state at the end of
     that step (acceptor records, log digests, proposer states, messages in
@@ -902,7 +932,8 @@ def test_trace_matches_oracle_steps(gpu_lib, c, inst):
     assert list(gres) == [res.decided_val, res.decided_ticket, res.rounds, res.packed_flags()]
 
 
-@pytest.mark.parametrize("c,inst", [(3, 0), (3, 17), (4, 5), (4, 123456), (5, 9), (5, 1000), (4, 77), (3, 4242)])
+@pytest.mark.parametrize("c,inst", [(3, 0), (3, 17), (4, 5), (4, 123456), (5, 9), (5, 1000), (4, 77), (3, 4242),
+                                    (7, 3), (7, 2024), (7, 555)])
 def test_trace_production_variant_matches_oracle_steps(gpu_lib, c, inst):
     """The carry-over variant the batch kernels run (a step may end with the
     copies of its last broadcast still to send): at every step it records, the
@@ -949,11 +980,8 @@ def test_log_mode_per_lane_matches_general_kernel(gpu_lib, cfg):
     the general LOGM kernel); the general kernel alone (PXB_NO_EV=1) and the
     oracle give identical results, digests, acceptor records and totals."""
     a = pxb.run(cfg, 99, 40000, want_acceptors=True)
-    os.environ["PXB_NO_EV"] = "1"
-    try:
+    with pxb.hooks(PXB_NO_EV="1"):
         b = pxb.run(cfg, 99, 40000, want_acceptors=True)
-    finally:
-        del os.environ["PXB_NO_EV"]
     for x, y in zip(a[:3], b[:3]):
         assert np.array_equal(x, y)
     assert a[3] == b[3]
@@ -984,8 +1012,8 @@ def test_step_kats_on_gpu(gpu_lib, case, production):
         for v in log:
             h = _fnv(h, v)
         assert int(dig[0][a]) == _fnv(h, len(log))
-    if cfg.n_ticks > 1:
-        return       # (pxb_trace_instance runs single decree only: results and records above)
+    # (log mode too, ABI 5: S4's Q5 double execution and S5's Q7 stale
+    # execution are pinned step by step, not only in the final records)
     recs, tres = pxb.trace_instance(cfg, case["instance"], production=production)
     assert list(tres) == list(res[0])
     steps = [r["step"] for r in recs]

@@ -46,7 +46,9 @@ def main():
             k, _, v = kv.partition("=")
             os.environ[k] = v
         pxb._lib = None
-        pxb.load(os.path.join(ROOT, lib))
+        lib_h = pxb.load(os.path.join(ROOT, lib))
+        if hasattr(lib_h, "pxb_reload_hooks"):       # (ABI >= 5: hooks are read once; re-read them)
+            lib_h.pxb_reload_hooks()
         row = []
         for c, n, reps in CASES:
             ms, t = timeit(pxb.CONFIGS[c], n, reps)

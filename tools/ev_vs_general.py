@@ -35,6 +35,7 @@ for name, cfg in CASES.items():
         for k in ("PXB_NO_EV", "PXB_NO_SPLIT"):
             os.environ.pop(k, None)
         os.environ.update(env)
+        pxb.reload_hooks()
         pxb.run_device(cfg, 1 << 36, 1 << 16, d_totals=tot)        # warm
         torch.cuda.synchronize()
         t0 = time.perf_counter()

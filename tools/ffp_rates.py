@@ -22,6 +22,7 @@ for name, (cfg, n) in CASES.items():
     for mode, env in (("per_lane", {}), ("general", {"PXB_NO_FFP": "1"})):
         os.environ.pop("PXB_NO_FFP", None)
         os.environ.update(env)
+        pxb.reload_hooks()
         pxb.run_device(cfg, 1 << 36, 1 << 16, d_totals=tot)
         torch.cuda.synchronize()
         tot.zero_()

@@ -143,7 +143,13 @@ int main(int argc, char** argv) {
   } else if (c == 4) {
     cfg.seed = 0x5EED0004; cfg.n_proposers = 2; cfg.n_acceptors = 7; cfg.delay_max = 4;
     cfg.crash_ppm = 200000; cfg.crash_len_max = 16; cfg.crash_start_max = 8; cfg.step_cap = 256;
-    if (getenv("TIGHT")) model<2, 7, 4, true, false, false, 2>(&cfg, n, rmin);   // layout 7 (tight)
+    // (NACC=6 / 8: the other topologies the tight routing may take, P = 2, N * P <= 16)
+    const int na = getenv("NACC") ? atoi(getenv("NACC")) : 7;
+    cfg.n_acceptors = (uint32_t)na;
+    const bool t = getenv("TIGHT") != nullptr;
+    if (na == 6) t ? model<2, 6, 4, true, false, false, 2>(&cfg, n, rmin) : model<2, 6, 4, true, false, false, 1>(&cfg, n, rmin);
+    else if (na == 8) t ? model<2, 8, 4, true, false, false, 2>(&cfg, n, rmin) : model<2, 8, 4, true, false, false, 1>(&cfg, n, rmin);
+    else if (t) model<2, 7, 4, true, false, false, 2>(&cfg, n, rmin);   // layout 7 (tight)
     else model<2, 7, 4, true, false, false, 1>(&cfg, n, rmin);   // layout 6 (simple schedule)
   } else if (c == 5) {
     // the three-proposer slim shape over every instance (P <= 3 drawn per instance)
