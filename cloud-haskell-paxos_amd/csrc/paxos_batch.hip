@@ -40,6 +40,14 @@ PXB_EV_FOR(PXB_EV_EXTERN, 2, 8, false) PXB_EV_FOR(PXB_EV_EXTERN, 2, 16, false) P
 PXB_EV_FOR(PXB_EV_EXTERN, 3, 8, false) PXB_EV_FOR(PXB_EV_EXTERN, 3, 16, false) PXB_EV_FOR(PXB_EV_EXTERN, 3, 8, true)
 #define PXB_EV_EXTERN_SL(PM, N, W, C) extern template __global__ void ev::paxos_ev_kernel<PM, N, W, C, false, true>(ev::EvKParams);
 PXB_EV_FOR(PXB_EV_EXTERN_SL, 1, 8, false) PXB_EV_FOR(PXB_EV_EXTERN_SL, 2, 8, false) PXB_EV_FOR(PXB_EV_EXTERN_SL, 3, 8, false)
+// (the compact 4-step, log-mode and simple-schedule shapes: instantiated in paxos_ev.hip too)
+PXB_EV_FOR(PXB_EV_EXTERN, 1, 4, true) PXB_EV_FOR(PXB_EV_EXTERN, 2, 4, true) PXB_EV_FOR(PXB_EV_EXTERN, 3, 4, true)
+#define PXB_EV_EXTERN_LG(PM, N, W, C) extern template __global__ void ev::paxos_ev_kernel<PM, N, W, C, true>(ev::EvKParams);
+PXB_EV_FOR(PXB_EV_EXTERN_LG, 1, 8, false) PXB_EV_FOR(PXB_EV_EXTERN_LG, 2, 8, false) PXB_EV_FOR(PXB_EV_EXTERN_LG, 3, 8, false)
+PXB_EV_FOR(PXB_EV_EXTERN_LG, 1, 16, false) PXB_EV_FOR(PXB_EV_EXTERN_LG, 2, 16, false) PXB_EV_FOR(PXB_EV_EXTERN_LG, 3, 16, false)
+#define PXB_EV_EXTERN_SP(PM, N, W, SP) extern template __global__ void ev::paxos_ev_kernel<PM, N, W, true, false, false, SP>(ev::EvKParams);
+PXB_EV_FOR(PXB_EV_EXTERN_SP, 1, 4, 1) PXB_EV_FOR(PXB_EV_EXTERN_SP, 2, 4, 1) PXB_EV_FOR(PXB_EV_EXTERN_SP, 3, 4, 1)
+PXB_EV_FOR(PXB_EV_EXTERN_SP, 2, 4, 2)
 #define PXB_FF1_EXTERN(N) extern template __global__ void ff1::paxos_ff1_kernel<N>(ff1::Ff1Params);
 PXB_FF1_EXTERN(2) PXB_FF1_EXTERN(3) PXB_FF1_EXTERN(4) PXB_FF1_EXTERN(5)
 PXB_FF1_EXTERN(6) PXB_FF1_EXTERN(7) PXB_FF1_EXTERN(8) PXB_FF1_EXTERN(9)
@@ -185,7 +193,9 @@ static ffp_kernel_ptr ffp_pick(uint32_t p, uint32_t n) {
 // layout index: 0 = 8-step wheel, 1 = 16-step wheel, 2 / 3 = compact links (8- / 4-step wheel),
 // 4 = log mode (8-step wheel), 5 = slim (8-step wheel, byte reply seqs), 6 = layout 3 for
 // simple schedules (no loss, no Tick skew: ev::layout_for), 7 = layout 6 with halfword
-// response FIFOs (tight: the first launch of the two-proposer simple schedules, P = 2 only)
+// response FIFOs (tight: the first launch of the two-proposer simple schedules, P = 2 only),
+// 8 = log mode on the 16-step wheel with its topology's larger pool (the second stage
+// behind layout 4 over <= 10 links)
 static ev_kernel_ptr ev_pick(uint32_t pm, uint32_t n, int layout) {
   switch (pm * 10 + (uint32_t)layout) {
     case 10: return ev_pick_n<1, 8, false>(n);
@@ -195,6 +205,7 @@ static ev_kernel_ptr ev_pick(uint32_t pm, uint32_t n, int layout) {
     case 14: return ev_pick_n<1, 8, false, true>(n);
     case 15: return ev_pick_n<1, 8, false, false, true>(n);
     case 16: return ev_pick_n<1, 4, true, false, false, 1>(n);
+    case 18: return ev_pick_n<1, 16, false, true>(n);
     case 20: return ev_pick_n<2, 8, false>(n);
     case 21: return ev_pick_n<2, 16, false>(n);
     case 22: return ev_pick_n<2, 8, true>(n);
@@ -203,6 +214,7 @@ static ev_kernel_ptr ev_pick(uint32_t pm, uint32_t n, int layout) {
     case 25: return ev_pick_n<2, 8, false, false, true>(n);
     case 26: return ev_pick_n<2, 4, true, false, false, 1>(n);
     case 27: return ev_pick_n<2, 4, true, false, false, 2>(n);
+    case 28: return ev_pick_n<2, 16, false, true>(n);
     case 30: return ev_pick_n<3, 8, false>(n);
     case 31: return ev_pick_n<3, 16, false>(n);
     case 32: return ev_pick_n<3, 8, true>(n);
@@ -210,6 +222,7 @@ static ev_kernel_ptr ev_pick(uint32_t pm, uint32_t n, int layout) {
     case 34: return ev_pick_n<3, 8, false, true>(n);
     case 35: return ev_pick_n<3, 8, false, false, true>(n);
     case 36: return ev_pick_n<3, 4, true, false, false, 1>(n);
+    case 38: return ev_pick_n<3, 16, false, true>(n);
   }
   return nullptr;
 }
@@ -259,7 +272,7 @@ static kernel_fn pick(uint32_t pm, uint32_t n, bool logm, bool ff) {
 // which is not safe against a concurrent setenv (tests/conftest.py's
 // `hooks` helper sets them and reloads)
 struct Hooks {
-  bool no_ev, no_ff1, no_ffp, no_split, no_tight, fail_after_first, ff1_bail;
+  bool no_ev, no_ff1, no_ffp, no_split, no_tight, no_lg2, fail_after_first, ff1_bail;
   int bail_cap;                   // PXB_EV_BAIL_CAP (-1: the default)
   int blocks_per_cu;              // PXB_BLOCKS_PER_CU (0: none)
   int ff1_oversub, ffp_oversub;   // PXB_FF1_OVERSUB / PXB_FFP_OVERSUB (0: FF1_OVERSUB)
@@ -344,7 +357,7 @@ struct EvLists {
 };
 static EvLists g_lists[64][EV_LIST_STREAMS];
 static int g_nlists[64], g_lnext[64];
-static int g_eocc[8][4][10][64];
+static int g_eocc[10][4][10][64];
 static int g_ff1occ[10][64];
 static int g_ffpocc[4][10][64];
 
@@ -530,6 +543,7 @@ static void read_hooks_locked() {
   h.no_ffp = flag("PXB_NO_FFP");
   h.no_split = flag("PXB_NO_SPLIT");
   h.no_tight = flag("PXB_NO_TIGHT");
+  h.no_lg2 = flag("PXB_NO_LG2");
   h.fail_after_first = flag("PXB_FAIL_AFTER_FIRST");
   h.ff1_bail = flag("PXB_FF1_BAIL");
   h.bail_cap = num("PXB_EV_BAIL_CAP", -1);
@@ -705,7 +719,19 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
   const ffp_kernel_ptr pfn = use_ffp ? ffp_pick(cfg->n_proposers, cfg->n_acceptors) : nullptr;
   if (use_ffp && !pfn) return PXB_E_INVAL;
   const int layout = ev::layout_for(cfg);
-  const ev_kernel_ptr efn = use_ev ? ev_pick(cfg->n_proposers, cfg->n_acceptors, layout) : nullptr;
+  // Two-stage faulty log mode over <= 10 links: the log-mode shape (layout 4,
+  // a 19-word response pool: 86 words, 7 waves per CU) over the chunk, the
+  // same shape on the 16-step wheel with a 32-word pool (layout 8) over what
+  // it hands on (pool overflows: none in 4 million instances of
+  // extra.log_mode_faulty, host model; 2 per million with an 18-word pool),
+  // the general log-mode kernel over that one's.  A handed-on instance is one
+  // of the longest; on the general kernel it held a 2^20-instance call 4-5 ms
+  // and a 2^22 one up to 22 ms after the per-lane kernel, on layout 8 0.9-6 ms
+  // (kernel traces, profiles/r06_notes/lg_kernel_trace.txt,
+  // lg2_kernel_trace_2p20.txt).  PXB_NO_LG2=1 turns it off.
+  const bool may_lg2 = use_ev && layout == 4 && cfg->n_proposers * cfg->n_acceptors <= 10 && !hk.no_lg2;
+  const int elayout = may_lg2 ? 8 : layout;
+  const ev_kernel_ptr efn = use_ev ? ev_pick(cfg->n_proposers, cfg->n_acceptors, elayout) : nullptr;
   if (use_ev && !efn) return PXB_E_INVAL;
   // Split routing of fuzzed three-proposer batches (config 5): the
   // two-proposer shape's layout fits more waves (config 5: 6 vs 4 per CU), so
@@ -731,7 +757,8 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
   const bool may_tight = use_ev && layout == 6 && cfg->n_proposers == 2 && cfg->n_acceptors >= 6 &&
                          cfg->n_acceptors <= 7 && !hk.no_tight;
   const ev_kernel_ptr sfn = may_split ? ev_pick(2, cfg->n_acceptors, layout)
-                            : may_tight ? ev_pick(2, cfg->n_acceptors, 7) : nullptr;
+                            : may_tight ? ev_pick(2, cfg->n_acceptors, 7)
+                            : may_lg2 ? ev_pick(cfg->n_proposers, cfg->n_acceptors, layout) : nullptr;
   // (split: the two-stage routing of either kind)
   bool split = false;
   const hipStream_t st = (hipStream_t)stream;
@@ -785,10 +812,10 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
       eocc = fo;
     }
     if (use_ev) {
-      if (int rc2 = ev_occ(efn, cfg->n_proposers, layout, &eocc)) return rc2;
+      if (int rc2 = ev_occ(efn, cfg->n_proposers, elayout, &eocc)) return rc2;
       if (sfn) {
-        if (int rc2 = ev_occ(sfn, 2, may_tight ? 7 : layout, &socc)) return rc2;
-        split = socc > eocc;
+        if (int rc2 = ev_occ(sfn, may_lg2 ? cfg->n_proposers : 2, may_tight ? 7 : layout, &socc)) return rc2;
+        split = may_lg2 || socc > eocc;
       }
     }
     if (hk.blocks_per_cu > 0) {                 // tests / experiments: cap residency
@@ -838,7 +865,8 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
   // fault-free log mode: 16-bit epochs, so every block's range (static slices:
   // every wave's) stays below 2^16 instances
   // (tight: bails are rare, so whole chunks; the list holds a quarter of one)
-  const uint64_t ev_chunk = (split && !may_tight) ? EV_SPLIT_CHUNK : EV_CHUNK;
+  // (log mode's second stage too)
+  const uint64_t ev_chunk = (split && !may_tight && !may_lg2) ? EV_SPLIT_CHUNK : EV_CHUNK;
   // fault-free per-lane kernels: as few launches as the general faulty kernel
   // allows (it may have to re-run a whole chunk); A/B on config 2 at 2^26:
   // 2^24-instance launches 2 % slower, 2^22 10 %, 2^20 33 %

@@ -193,7 +193,7 @@ struct Shape {
 // waves per CU instead of 4), 86 for P = 2 (7 instead of 6).
 // Log mode (LG) carries commands "c<id>.<t>" as 14 bits, id [13:12] | t [11:0]
 // (t >= 1; 0 = Nothing) and keeps 4 broadcast ring slots per proposer (with
-// the 18-word response pool of topologies of <= 10 links, EvPool: 85 words per
+// the 19-word response pool of topologies of <= 10 links, EvPool: 86 words per
 // lane for P = 2, N = 5, 7 waves per CU), so:
 //   acceptor word       t_max [11:0] | t_store [23:12] | dead [24]; a second word (accv):
 //                       the stored command [13:0] | log_len [31:14]
@@ -1391,10 +1391,14 @@ __host__ inline int layout_for(const pxb_config* c) {
 #endif
   return 0;
 }
-__host__ inline int layout_wheel(int layout) { return layout == 1 ? 16 : (layout == 3 || layout == 6 || layout == 7) ? 4 : 8; }
+__host__ inline int layout_wheel(int layout) {
+  return (layout == 1 || layout == 8) ? 16 : (layout == 3 || layout == 6 || layout == 7) ? 4 : 8;
+}
 __host__ inline bool layout_compact(int layout) { return layout == 2 || layout == 3 || layout == 6 || layout == 7; }
 __host__ inline bool layout_simple(int layout) { return layout == 6 || layout == 7; }
-__host__ inline bool layout_log(int layout) { return layout == 4; }
+// (8: layout 4 on the 16-step wheel with its topology's larger pool, the
+// second stage of two-stage log mode, pxb_run_device)
+__host__ inline bool layout_log(int layout) { return layout == 4 || layout == 8; }
 
 }  // namespace ev
 }  // namespace pxb

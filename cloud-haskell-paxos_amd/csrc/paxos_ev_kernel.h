@@ -77,9 +77,13 @@ struct EvKParams {
 #ifndef PXB_EV_CMP_POOL
 #define PXB_EV_CMP_POOL 24
 #endif
-// (log mode over at most 10 links: 18 words, which faulty log mode's batch never
-// fills (extra.log_mode_faulty: no bail in 20000 instances): 85 words per lane,
-// 7 waves per CU instead of 5.  Round 5 measured the halfword response links
+// (log mode over at most 10 links: 19 words, 86 per lane, 7 waves per CU instead
+// of 5 (9.5 KiB of LDS to spare).  Round 6: with 18 words (85 per lane) faulty
+// log mode handed on 2 instances per million (host model), one of the
+// longest each time, so nearly every 2^20-instance call waited 4-5 ms for its
+// re-run after the per-lane kernel (kernel trace,
+// profiles/r06_notes/lg2_kernel_trace_2p20.txt); with 19, none in 4 million.
+// Round 5 measured the halfword response links
 // here too (PXB_EV_LG_RH=1 with PXB_EV_LG_POOL=15: 75 words, 8 waves per CU,
 // 9 bails in 20000): 2^22 +-1 %, 2^20 -11 % (the chunk tail): not used)
 // (slim: 44 words hold the responses of 99.6 % of config 5's P = 3 instances
@@ -100,15 +104,17 @@ struct EvKParams {
 #define PXB_EV_SL2_POOL 28
 #endif
 #ifndef PXB_EV_LG_POOL
-#define PXB_EV_LG_POOL 18
+#define PXB_EV_LG_POOL 19
 #endif
 #ifndef PXB_EV_TIGHT_POOL
 #define PXB_EV_TIGHT_POOL 21
 #endif
-template <int PM, int N, bool CMP, bool LG = false, bool SL = false, int SP = 0>
+// (W: the log-mode shape on the 16-step wheel, the second stage behind the
+// 8-step one, takes the larger pool of its topology)
+template <int PM, int N, bool CMP, bool LG = false, bool SL = false, int SP = 0, int W = 8>
 struct EvPool {
   static constexpr int value = (SP == 2)             ? PXB_EV_TIGHT_POOL
-                               : (LG && PM * N <= 10)  ? PXB_EV_LG_POOL
+                               : (LG && PM * N <= 10 && W == 8) ? PXB_EV_LG_POOL
                                : (CMP && PM * N <= 10) ? 16
                                : (PM * N <= 16)      ? (CMP ? PXB_EV_CMP_POOL : 32)
                                : CMP                ? PXB_EV_CMPW_POOL
@@ -163,7 +169,7 @@ struct EvTotals {
 // The slim layout fits 5 or more waves per CU, 2 on some SIMDs: <= 256 VGPRs.
 template <int PM, int N, int W, bool CMP, bool LG = false, bool SL = false, int SP = 0>
 __global__ __launch_bounds__(64, CMP ? 3 : SL ? 2 : 1) void paxos_ev_kernel(EvKParams kp) {
-  constexpr int POOL = EvPool<PM, N, CMP, LG, SL, SP>::value;
+  constexpr int POOL = EvPool<PM, N, CMP, LG, SL, SP, W>::value;
   using S = Shape<PM, N, POOL, W, CMP, LG, SL, SP>;
   __shared__ uint32_t lds[S::WORDS * 64];
   const uint32_t lane = threadIdx.x;

@@ -63,7 +63,7 @@ struct HostMem {
 template <int PM, int N, int W, bool CMP, bool LG, bool SL, int SP>
 int run_shape(const pxb_config* cfg, pxb_result* out, uint32_t* dig, pxb_acceptor_rec* acc, int64_t* tot,
               uint32_t* bail_ids, uint32_t* n_bail, uint64_t* micro_steps) {
-  constexpr int POOL = EvPool<PM, N, CMP, LG, SL, SP>::value;
+  constexpr int POOL = EvPool<PM, N, CMP, LG, SL, SP, W>::value;
   using S = Shape<PM, N, POOL, W, CMP, LG, SL, SP>;
   g_words = S::WORDS;
   // garbage: init must set what it reads (checked builds: exactly WORDS, so
@@ -175,7 +175,7 @@ extern "C" int ev_host_run(const pxb_config* cfg, pxb_result* out, uint32_t* dig
   if (layout == 2 && cfg->delay_max > 8) return -1;
   if ((layout == 3 || layout == 6 || layout == 7) && cfg->delay_max > 4) return -1;
   if ((layout == 6 || layout == 7) && (cfg->loss_ppm || cfg->skew_max || (cfg->flags & PXB_CFG_RANDOMIZE) || cfg->n_ticks > 1)) return -1;
-  if ((layout == 4) != (cfg->n_ticks > 1)) return -1;      // log mode runs on the log-mode fields only
+  if ((layout == 4 || layout == 8) != (cfg->n_ticks > 1)) return -1;   // log mode runs on the log-mode fields only
   if ((layout == 0 || layout == 5) && cfg->delay_max > 8) return -1;
   // tests: the shape's proposer capacity; below n_proposers (fuzzed batches
   // only) it is the split routing of pxb_run_device, whose instances with more
@@ -195,6 +195,7 @@ extern "C" int ev_host_run(const pxb_config* cfg, pxb_result* out, uint32_t* dig
     case 5: return run_w<8, false, false, true>(cfg, pm, out, dig, acc, totals, bail_ids, n_bail, micro_steps);
     case 6: return run_w<4, true, false, false, 1>(cfg, pm, out, dig, acc, totals, bail_ids, n_bail, micro_steps);
     case 7: return run_w<4, true, false, false, 2>(cfg, pm, out, dig, acc, totals, bail_ids, n_bail, micro_steps);
+    case 8: return run_w<16, false, true>(cfg, pm, out, dig, acc, totals, bail_ids, n_bail, micro_steps);
   }
   return -1;
 }

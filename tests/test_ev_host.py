@@ -257,7 +257,25 @@ def test_log_mode(P, N, loss, delay, ticks, period, crash):
     assert cnt["executes"] >= cnt["decided"]
 
 
-@pytest.mark.parametrize("P,loss,crash,period,delay,clen", [(1, 10000, 150000, 8, 2, 20), (2, 0, 100000, 12, 1, 30)])
+@pytest.mark.parametrize("P,N,loss,delay,ticks,period,crash", [
+    (2, 5, 100000, 4, 16, 8, 200000),    # faulty log mode (BASELINE-like, extra.log_mode_faulty)
+    (1, 9, 300000, 8, 10, 3, 300000),
+    (3, 3, 200000, 6, 12, 5, 100000),
+    (2, 2, 0, 1, 16, 8, 0)])
+def test_log_mode_second_stage_layout(P, N, loss, delay, ticks, period, crash, monkeypatch):
+    """Layout 8, the log-mode shape on the 16-step wheel with its topology's
+    larger pool (32 words over <= 10 links): the second stage of two-stage
+    faulty log mode (pxb_run_device re-runs the first stage's hand-offs on
+    it).  Exact against the oracle, and it hands on nothing here."""
+    monkeypatch.setenv("EV_LAYOUT", "8")
+    cfg = pxb.Config(seed=0x1C8 + 16 * P + N, n_proposers=P, n_acceptors=N, loss_ppm=loss,
+                     delay_max=delay, skew_max=3, crash_ppm=crash, crash_len_max=12,
+                     crash_start_max=30, step_cap=1024, n_ticks=ticks, tick_period=period)
+    _, cnt, bails = check(cfg, 77, 1500, max_bail_frac=0.0)
+    assert cnt["executes"] >= cnt["decided"] and len(bails) == 0
+
+
+@pytest.mark.parametrize("P,loss,crash,period,delay,clen",[(1, 10000, 150000, 8, 2, 20), (2, 0, 100000, 12, 1, 30)])
 def test_log_mode_past_log_track(P, loss, crash, period, delay, clen):
     """100 Ticks per proposer: logs past LOG_TRACK = 32 set LOG_TRUNC; the
     divergence check covers the first 32 positions (as the oracle's)."""
@@ -296,7 +314,7 @@ def test_random_log_mode_schedules(i):
     (3, 2, 44, 12),      # compact, 16-word pool (12 = the VGPR limit)
     (5, 3, 120, 5),      # slim, P = 3 share
     (5, 2, 75, 8),       # slim, P <= 2 share (halfword response links, 28-word pool)
-    (7, 2, 85, 7),       # faulty log mode
+    (7, 2, 86, 7),       # faulty log mode (19-word pool)
 ])
 def test_layout_words_leave_lds_to_spare(c, pm, words, blocks, monkeypatch):
     if c < 0:

@@ -971,6 +971,43 @@ def test_trace_production_variant_matches_oracle_steps(gpu_lib, c, inst):
     assert list(gres) == [res.decided_val, res.decided_ticket, res.rounds, res.packed_flags()]
 
 
+def test_log_mode_two_stage_routing(gpu_lib):
+    """Faulty log mode over <= 10 links runs in two per-lane stages: the
+    log-mode shape (18-word pool) over the chunk, the same shape on the 16-step
+    wheel with a 32-word pool over what it hands on, the general log-mode
+    kernel over that one's.  A schedule whose responses pile up (delays to 8,
+    no loss, a Tick every 2 steps: ~0.15 % stage-1 hand-offs, host model):
+    stage 1 hands >= 20 on, stage 2 nearly none; results, digests, acceptor
+    records and totals equal the oracle's, the one-stage routing's
+    (PXB_NO_LG2=1) and, with the id lists capped (0: the first list overflows,
+    so the general kernel re-runs the chunk; 3: either may), the same again."""
+    cfg = pxb.Config(seed=0x7C, n_proposers=2, n_acceptors=5, delay_max=8, skew_max=3, step_cap=1024,
+                     n_ticks=16, tick_period=2)
+    first, n = 1 << 35, 60000
+    pxb.handoff_counts(0, reset=True)
+    _cmp(cfg, first, n)
+    h1, h2 = pxb.handoff_counts(0, reset=True)
+    assert h1 >= 20 and h2 <= h1 // 4, (h1, h2)
+    a = pxb.run(cfg, first, n, want_acceptors=True)
+    for env in ({"PXB_NO_LG2": "1"}, {"PXB_EV_BAIL_CAP": "0"}, {"PXB_EV_BAIL_CAP": "3"}):
+        b = _with_env(env, lambda: pxb.run(cfg, first, n, want_acceptors=True))
+        for x, y in zip(a[:3], b[:3]):
+            assert np.array_equal(x, y), env
+        assert a[3] == b[3], env
+
+
+def test_log_mode_contiguous_faulty_config(gpu_lib):
+    """2^21 contiguous faulty-log-mode instances (pxb.LOG_FAULTY_CONFIG, the
+    bench's log_mode_faulty) through the two-stage routing, bit-exact against
+    the oracle: results, digests and totals."""
+    cfg, first, n = pxb.LOG_FAULTY_CONFIG, 5 << 33, 1 << 21
+    eres, edig, _, ecnt = oracle_c.run_cpu(cfg, first, n, threads=THREADS)
+    res, dig, _, cnt = pxb.run(cfg, first, n)
+    bad = np.nonzero((res != eres).any(axis=1))[0]
+    assert bad.size == 0, "first mismatch at %d" % (first + bad[0])
+    assert np.array_equal(dig, edig) and cnt == ecnt
+
+
 @pytest.mark.parametrize("cfg", [pxb.LOG_FAULTY_CONFIG, pxb.Config(seed=0x10E, n_proposers=3, n_acceptors=9, loss_ppm=300000,
                                                         delay_max=8, skew_max=3, crash_ppm=200000,
                                                         crash_len_max=16, crash_start_max=16, step_cap=512,

@@ -14,6 +14,8 @@
 #   ab:<lib.so>+<lib.so>...    tools/ab_ev.py A/B of library variants (AB_CASES, AB_PASSES from the env)
 #   prof:<config>,<n>,<steps>,<warmup>[,<round>]   tools/profile_set.sh -> profiles/<round>_config<c>
 #   wt:<lib.so>,<config>,<n>   per-wave timelines (tools/ev_wave_times.py, a -DPXB_WAVE_TIMES build)
+#   env:<VAR>=<value>          set a library hook (PXB_NO_LG2=1, ...) for the steps after it
+#   unenv:<VAR>                unset it again
 # Output: gpurun_out/<tag>/ (step logs, bench JSON lines, profiles).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -63,6 +65,8 @@ for step in "$@"; do
       IFS=, read -r lib c n <<< "$arg"
       timeout -k 10 300 python3 -u tools/ev_wave_times.py $lib $c $n > $O/wt_$k.txt 2>&1 || { tail -20 $O/wt_$k.txt; exit 1; }
       cat $O/wt_$k.txt ;;
+    env) export "$arg" ;;
+    unenv) unset "$arg" ;;
     *) echo "unknown step $step"; exit 1 ;;
   esac
 done

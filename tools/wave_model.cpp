@@ -43,9 +43,13 @@ struct HostMem {
 constexpr int NB = 10;
 const char* names[NB] = {"END", "FIN", "RUN", "TICK_ENTER", "TICK_END", "ACC", "PROP", "COPY", "SEND1", "BCAST"};
 
+// (ids: run only these instances, as a second-stage kernel over another's
+// hand-offs; bailed_out: the ids this shape hands on)
 template <int PM, int N, int W, bool CMP, bool LG, bool SL, int SP = 0>
-void model(const pxb_config* cfg, uint32_t n, uint32_t refill_min) {
-  constexpr int POOL = EvPool<PM, N, CMP, LG, SL, SP>::value;
+void model(const pxb_config* cfg, uint32_t n, uint32_t refill_min, const std::vector<uint32_t>* ids = nullptr,
+           std::vector<uint32_t>* bailed_out = nullptr) {
+  if (ids) n = (uint32_t)ids->size();
+  constexpr int POOL = EvPool<PM, N, CMP, LG, SL, SP, W>::value;
   using S = Shape<PM, N, POOL, W, CMP, LG, SL, SP>;
   const EvParams p = make_params(cfg);
   using Lane = EvLane<PM, N, POOL, W, CMP, HostMem, true, LG, SL, SP>;
@@ -68,9 +72,11 @@ void model(const pxb_config* cfg, uint32_t n, uint32_t refill_min) {
       ++refills;
       for (int l = 0; l < 64 && next < n; ++l)
         if (L[l].mode == M_IDLE) {
-          L[l].init(p, next++);
+          L[l].init(p, ids ? (*ids)[next] : next);
+          ++next;
           ++inits;
           if (L[l].bailed) {
+            if (bailed_out) bailed_out->push_back(L[l].gid);
             L[l].mode = M_IDLE;
             L[l].bailed = false;
             ++bails;
@@ -95,6 +101,7 @@ void model(const pxb_config* cfg, uint32_t n, uint32_t refill_min) {
       orb |= ev_probe_bits;
       for (int b = 0; b < NB; ++b) sum[b] += (ev_probe_bits >> b) & 1u;
       if (L[l].bailed) {
+        if (bailed_out) bailed_out->push_back(L[l].gid);
         for (int b = 0; b < 6; ++b) bcause[b] += (ev_probe_bits >> (16 + b)) & 1u;
         L[l].mode = M_IDLE;
         L[l].bailed = false;
@@ -160,14 +167,31 @@ int main(int argc, char** argv) {
       cfg.delay_max = 4;
       model<3, 9, 4, true, false, false>(&cfg, n, rmin);
     } else {
-      model<3, 9, 8, false, false, true>(&cfg, n, rmin);
+      std::vector<uint32_t> bailed;
+      model<3, 9, 8, false, false, true>(&cfg, n, rmin, nullptr, &bailed);
+      if (getenv("STAGE2")) {   // a third per-lane stage over the P = 3 shape's hand-offs: layout 0 / 1
+        std::vector<uint32_t> p3;
+        for (uint32_t g : bailed) p3.push_back(g);
+        printf("-- layout 0 over %zu hand-offs\n", p3.size());
+        std::vector<uint32_t> b2, b3;
+        model<3, 9, 8, false, false, false>(&cfg, 0, rmin, &p3, &b2);
+        printf("-- layout 1 over %zu hand-offs\n", p3.size());
+        model<3, 9, 16, false, false, false>(&cfg, 0, rmin, &p3, &b3);
+      }
     }
   } else if (c == 7) {
     // faulty log mode (pxb.LOG_FAULTY_CONFIG): the LG shape, layout 4
     cfg.seed = 0x5EED0007; cfg.n_proposers = 2; cfg.n_acceptors = 5; cfg.loss_ppm = 100000;
     cfg.delay_max = 4; cfg.skew_max = 3; cfg.crash_ppm = 200000; cfg.crash_len_max = 16;
     cfg.crash_start_max = 64; cfg.step_cap = 1024; cfg.n_ticks = 16; cfg.tick_period = 8;
-    model<2, 5, 8, false, true, false>(&cfg, n, rmin);
+    std::vector<uint32_t> bailed;
+    model<2, 5, 8, false, true, false>(&cfg, n, rmin, nullptr, &bailed);
+    if (getenv("STAGE2")) {   // the LG shape on the 16-step wheel (its larger pool) over the hand-offs
+      printf("-- second stage over %zu hand-offs\n", bailed.size());
+      std::vector<uint32_t> b2;
+      model<2, 5, 16, false, true, false>(&cfg, 0, rmin, &bailed, &b2);
+      printf("-- still handed on: %zu\n", b2.size());
+    }
   } else {
     fprintf(stderr, "config 3, 4, 5 or 7\n");
     return 1;
