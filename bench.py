@@ -402,23 +402,34 @@ def faulty_line(name, c, n, steps, warmup, stream, dev, warm_n, rank=0, world=1,
     return line
 
 
+LOG_STEPS = 8                # timed steps of the faulty-log-mode lines (round 5: 2)
+
+
 def log_faulty_line(stream, dev, n=1 << 22, general=True):
     """Faulty log mode (pxb.LOG_FAULTY_CONFIG: P = 2, N = 5, 10 % loss, delays
     to 4, crash windows, 16 Ticks 8 steps apart) on the per-lane kernel's
     log-mode shape, and (general=True) the same batch on the general kernel
     (PXB_NO_EV=1) for the speed-up; the totals of the two must be identical.
-    At 2^22 instances per step the kernel runs saturated; at 2^20 the chunk
-    tail (the slowest instances of the last waves) is a large share."""
+    LOG_STEPS timed steps on the two step streams.  The batch's instance
+    lengths have a heavy tail (median 124 steps, the longest ~950: 7.7 x), so
+    a call's last waves run its longest instances for 2-5 ms after its work
+    queue drained (profiles/r06_notes/lg_wave_times_2p20.txt: at 2^20 the
+    queue drains at 5.0 ms and the last wave ends at 10.2 ms); consecutive
+    steps on two streams fill part of that tail, and one tail stays exposed
+    per measurement.  Round 5 timed 2 steps, so that exposed tail weighed 4x
+    more there (the 2-step rate is reported beside it)."""
     import pxb
     cfg = pxb.LOG_FAULTY_CONFIG
-    es, ek, ecnt = run_workload(GpuLeg(cfg, n, 0, 1, stream, dev), n, 2, 1, 1)
+    es, ek, ecnt = run_workload(GpuLeg(cfg, n, 0, 1, stream, dev), n, LOG_STEPS, 1, 1)
+    e2s, _, e2cnt = run_workload(GpuLeg(cfg, n, 0, 1, stream, dev), n, 2, 1, 1)
     line = {"workload": "faulty log mode: P=2, N=5, 10% loss, delay [1,4], crash windows, 16 Ticks / 8 steps",
-            "instances_per_step": n, "instances_per_s": ecnt["instances"] / es,
+            "instances_per_step": n, "steps": LOG_STEPS, "instances_per_s": ecnt["instances"] / es,
             "commands_committed_per_s": ecnt["executes"] / es, "kernel_ms": ek,
-            "roofline": roofline("config7", n, ek, ecnt["canon_bytes"] / 2), "counters": ecnt}
+            "instances_per_s_2_steps": e2cnt["instances"] / e2s,
+            "roofline": roofline("config7", n, ek, ecnt["canon_bytes"] / LOG_STEPS), "counters": ecnt}
     if general:
         with pxb.hooks(PXB_NO_EV="1"):
-            gs, gk, gcnt = run_workload(GpuLeg(cfg, n, 0, 1, stream, dev), n, 2, 1, 1)
+            gs, gk, gcnt = run_workload(GpuLeg(cfg, n, 0, 1, stream, dev), n, LOG_STEPS, 1, 1)
         assert gcnt == ecnt, (gcnt, ecnt)
         line["general_kernel"] = {"instances_per_s": gcnt["instances"] / gs, "kernel_ms": gk}
         line["speedup_vs_general_kernel"] = gk / ek

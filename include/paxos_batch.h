@@ -159,8 +159,10 @@ int pxb_run(const pxb_config* cfg, pxb_result* out, uint32_t* log_digest,
  *     and the three-proposer one over the instances that drew P = 3 (chunks
  *     of 2^26; 2^25 split);
  *   faulty log mode (n_ticks > 1, delays <= 8): the per-lane event kernel's
- *     log-mode shape, then the general log-mode kernel over its bailed
- *     instances (chunks of 2^26; longer delays: the general log-mode kernel).
+ *     log-mode shape, over <= 10 links the same shape on the 16-step wheel
+ *     with a larger pool over what it hands on, then the general log-mode
+ *     kernel over the rest (chunks of 2^26; longer delays: the general
+ *     log-mode kernel).
  * Each chunk
  * uses one of 64 per-device scratch slots round-robin; a chunk that takes a
  * slot makes its stream wait (on the device, hipStreamWaitEvent) for the
