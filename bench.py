@@ -42,7 +42,7 @@ HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip
 CUS = 256
 VALU_PEAK_G = CUS * 2 * 2.4  # G wave64 VALU instructions / s (1228.8)
 PROFILES = os.path.join(ROOT, "profiles")
-PROFILE_ROUNDS = ("r05", "r04", "r03", "r02")   # the newest committed profile set of a workload wins
+PROFILE_ROUNDS = ("r06", "r05", "r04", "r03", "r02")   # the newest committed profile set of a workload wins
 BATCHES_PER_STEP = 256       # config-2 batches of 2^20 per timed step (>= 100 ms over 20 steps)
 STEP_STREAMS = 0             # --streams (A/B; --one-stream = 1; 0: by step size, GpuLeg)
 DRY_NORTH_STAR = 1 << 12     # --dry-run stand-in for the headline's 2^26 instances per step
