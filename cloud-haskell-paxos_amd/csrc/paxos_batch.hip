@@ -45,6 +45,8 @@ PXB_EV_FOR(PXB_EV_EXTERN, 1, 4, true) PXB_EV_FOR(PXB_EV_EXTERN, 2, 4, true) PXB_
 #define PXB_EV_EXTERN_LG(PM, N, W, C) extern template __global__ void ev::paxos_ev_kernel<PM, N, W, C, true>(ev::EvKParams);
 PXB_EV_FOR(PXB_EV_EXTERN_LG, 1, 8, false) PXB_EV_FOR(PXB_EV_EXTERN_LG, 2, 8, false) PXB_EV_FOR(PXB_EV_EXTERN_LG, 3, 8, false)
 PXB_EV_FOR(PXB_EV_EXTERN_LG, 1, 16, false) PXB_EV_FOR(PXB_EV_EXTERN_LG, 2, 16, false) PXB_EV_FOR(PXB_EV_EXTERN_LG, 3, 16, false)
+#define PXB_EV_EXTERN_LGS(PM, N, W, C) extern template __global__ void ev::paxos_ev_kernel<PM, N, W, C, true, true>(ev::EvKParams);
+PXB_EV_FOR(PXB_EV_EXTERN_LGS, 1, 4, false) PXB_EV_FOR(PXB_EV_EXTERN_LGS, 2, 4, false) PXB_EV_FOR(PXB_EV_EXTERN_LGS, 3, 4, false)
 #define PXB_EV_EXTERN_SP(PM, N, W, SP) extern template __global__ void ev::paxos_ev_kernel<PM, N, W, true, false, false, SP>(ev::EvKParams);
 PXB_EV_FOR(PXB_EV_EXTERN_SP, 1, 4, 1) PXB_EV_FOR(PXB_EV_EXTERN_SP, 2, 4, 1) PXB_EV_FOR(PXB_EV_EXTERN_SP, 3, 4, 1)
 PXB_EV_FOR(PXB_EV_EXTERN_SP, 2, 4, 2)
@@ -195,7 +197,8 @@ static ffp_kernel_ptr ffp_pick(uint32_t p, uint32_t n) {
 // simple schedules (no loss, no Tick skew: ev::layout_for), 7 = layout 6 with halfword
 // response FIFOs (tight: the first launch of the two-proposer simple schedules, P = 2 only),
 // 8 = log mode on the 16-step wheel with its topology's larger pool (the second stage
-// behind layout 4 over <= 10 links)
+// behind layout 4 over <= 10 links), 9 = layout 4 slimmed (byte reply seqs in registers) on
+// the 4-step wheel (the first stage of log mode over <= 10 links with delays <= 4)
 static ev_kernel_ptr ev_pick(uint32_t pm, uint32_t n, int layout) {
   switch (pm * 10 + (uint32_t)layout) {
     case 10: return ev_pick_n<1, 8, false>(n);
@@ -206,6 +209,7 @@ static ev_kernel_ptr ev_pick(uint32_t pm, uint32_t n, int layout) {
     case 15: return ev_pick_n<1, 8, false, false, true>(n);
     case 16: return ev_pick_n<1, 4, true, false, false, 1>(n);
     case 18: return ev_pick_n<1, 16, false, true>(n);
+    case 19: return ev_pick_n<1, 4, false, true, true>(n);
     case 20: return ev_pick_n<2, 8, false>(n);
     case 21: return ev_pick_n<2, 16, false>(n);
     case 22: return ev_pick_n<2, 8, true>(n);
@@ -215,6 +219,7 @@ static ev_kernel_ptr ev_pick(uint32_t pm, uint32_t n, int layout) {
     case 26: return ev_pick_n<2, 4, true, false, false, 1>(n);
     case 27: return ev_pick_n<2, 4, true, false, false, 2>(n);
     case 28: return ev_pick_n<2, 16, false, true>(n);
+    case 29: return ev_pick_n<2, 4, false, true, true>(n);
     case 30: return ev_pick_n<3, 8, false>(n);
     case 31: return ev_pick_n<3, 16, false>(n);
     case 32: return ev_pick_n<3, 8, true>(n);
@@ -223,6 +228,7 @@ static ev_kernel_ptr ev_pick(uint32_t pm, uint32_t n, int layout) {
     case 35: return ev_pick_n<3, 8, false, false, true>(n);
     case 36: return ev_pick_n<3, 4, true, false, false, 1>(n);
     case 38: return ev_pick_n<3, 16, false, true>(n);
+    case 39: return ev_pick_n<3, 4, false, true, true>(n);
   }
   return nullptr;
 }
@@ -272,7 +278,7 @@ static kernel_fn pick(uint32_t pm, uint32_t n, bool logm, bool ff) {
 // which is not safe against a concurrent setenv (tests/conftest.py's
 // `hooks` helper sets them and reloads)
 struct Hooks {
-  bool no_ev, no_ff1, no_ffp, no_split, no_tight, no_lg2, fail_after_first, ff1_bail;
+  bool no_ev, no_ff1, no_ffp, no_split, no_tight, no_lg2, no_lgs, fail_after_first, ff1_bail;
   int bail_cap;                   // PXB_EV_BAIL_CAP (-1: the default)
   int blocks_per_cu;              // PXB_BLOCKS_PER_CU (0: none)
   int ff1_oversub, ffp_oversub;   // PXB_FF1_OVERSUB / PXB_FFP_OVERSUB (0: FF1_OVERSUB)
@@ -357,7 +363,7 @@ struct EvLists {
 };
 static EvLists g_lists[64][EV_LIST_STREAMS];
 static int g_nlists[64], g_lnext[64];
-static int g_eocc[10][4][10][64];
+static int g_eocc[11][4][10][64];
 static int g_ff1occ[10][64];
 static int g_ffpocc[4][10][64];
 
@@ -544,6 +550,7 @@ static void read_hooks_locked() {
   h.no_split = flag("PXB_NO_SPLIT");
   h.no_tight = flag("PXB_NO_TIGHT");
   h.no_lg2 = flag("PXB_NO_LG2");
+  h.no_lgs = flag("PXB_NO_LGS");
   h.fail_after_first = flag("PXB_FAIL_AFTER_FIRST");
   h.ff1_bail = flag("PXB_FF1_BAIL");
   h.bail_cap = num("PXB_EV_BAIL_CAP", -1);
@@ -730,7 +737,16 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
   // (kernel traces, profiles/r06_notes/lg_kernel_trace.txt,
   // lg2_kernel_trace_2p20.txt).  PXB_NO_LG2=1 turns it off.
   const bool may_lg2 = use_ev && layout == 4 && cfg->n_proposers * cfg->n_acceptors <= 10 && !hk.no_lg2;
-  const int elayout = may_lg2 ? 8 : layout;
+  // With delays <= 4 the first stage is layout 9: layout 4 with its reply seqs
+  // as bytes in registers, the 4-step wheel and its canonical log packed (14
+  // words), the same 19-word pool: 75 LDS words, 8 waves per CU instead of 7
+  // (residency sweep, faulty log mode at 2^22, PXB_BLOCKS_PER_CU 5 / 6 / 7:
+  // 32.7 / 29.6 / 27.5 ms; layout 9: 2^22 +5.6 %, 2^20 +2.5 %,
+  // profiles/r06_notes/ab_lg_layout9.txt).  PXB_NO_LGS=1 keeps layout 4.
+  const bool lgs = use_ev && layout == 4 && cfg->delay_max <= 4 && cfg->n_proposers * cfg->n_acceptors <= 10 &&
+                   !hk.no_lgs;
+  const int flayout = lgs ? 9 : layout;     // (the first per-lane stage's)
+  const int elayout = may_lg2 ? 8 : flayout;
   const ev_kernel_ptr efn = use_ev ? ev_pick(cfg->n_proposers, cfg->n_acceptors, elayout) : nullptr;
   if (use_ev && !efn) return PXB_E_INVAL;
   // Split routing of fuzzed three-proposer batches (config 5): the
@@ -758,7 +774,7 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
                          cfg->n_acceptors <= 7 && !hk.no_tight;
   const ev_kernel_ptr sfn = may_split ? ev_pick(2, cfg->n_acceptors, layout)
                             : may_tight ? ev_pick(2, cfg->n_acceptors, 7)
-                            : may_lg2 ? ev_pick(cfg->n_proposers, cfg->n_acceptors, layout) : nullptr;
+                            : may_lg2 ? ev_pick(cfg->n_proposers, cfg->n_acceptors, flayout) : nullptr;
   // (split: the two-stage routing of either kind)
   bool split = false;
   const hipStream_t st = (hipStream_t)stream;
@@ -814,7 +830,7 @@ int pxb_run_device(const pxb_config* cfg, pxb_result* d_out, uint32_t* d_log_dig
     if (use_ev) {
       if (int rc2 = ev_occ(efn, cfg->n_proposers, elayout, &eocc)) return rc2;
       if (sfn) {
-        if (int rc2 = ev_occ(sfn, may_lg2 ? cfg->n_proposers : 2, may_tight ? 7 : layout, &socc)) return rc2;
+        if (int rc2 = ev_occ(sfn, may_lg2 ? cfg->n_proposers : 2, may_tight ? 7 : flayout, &socc)) return rc2;
         split = may_lg2 || socc > eocc;
       }
     }

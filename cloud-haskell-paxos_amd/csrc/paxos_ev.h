@@ -154,7 +154,11 @@ struct Shape {
   static constexpr int POOLZ = POOLW + POOL;         // LG: POOL + 1 halfwords
   static constexpr int BRING = POOLZ + (LG ? POOL / 2 + 1 : 0);   // PM*BR payloads: halfwords (LG: words)
   static constexpr int CLOG = BRING + (LG ? PM * BR : PM * BR / 2);   // LG: PXB_LOG_TRACK halfwords
-  static constexpr int WHEEL = CLOG + (LG ? PXB_LOG_TRACK / 2 : 0);   // W * WW due masks
+  // (CLP: the slim log-mode shape packs its canonical log's 14-bit commands
+  // end to end, 14 words instead of 16)
+  static constexpr bool CLP = LG && SL;
+  static constexpr int CLW = !LG ? 0 : CLP ? (PXB_LOG_TRACK * 14 + 31) / 32 : PXB_LOG_TRACK / 2;
+  static constexpr int WHEEL = CLOG + CLW;           // W * WW due masks
   static constexpr int RSP = RH ? WHEEL + W * WW : RSP0;
   static constexpr int WORDS = WHEEL + W * WW + (RH ? (NLQ + 1) / 2 : 0);
   static_assert(W == 4 || W == 8 || W == 16, "wheel of 4, 8 or 16 steps");
@@ -1033,13 +1037,28 @@ struct EvLane {
         // 4 % of the lanes: nested exec-mask branches cost every one of them)
         const bool trk = log_len < (uint32_t)PXB_LOG_TRACK;
         const uint32_t li = trk ? log_len : (uint32_t)PXB_LOG_TRACK - 1u;
-        const uint32_t cw = S::CLOG + (li >> 1), ch = li & 1u;
-        const uint32_t old = m.ld16h(cw, ch);
         const bool seen = log_len < clog_len;
+        const bool app = trk & !seen;
+        uint32_t old;
+        if constexpr (S::CLP) {
+          // position li at bit 14 li of the packed words: a 64-bit window of
+          // words w and w + 1 (the last position ends at bit 32 of word CLW - 1,
+          // whose window is that word twice: stored high half first, low last)
+          const uint32_t b = mulc<14>(li), w = b >> 5, sh = b & 31u;
+          const uint32_t w1 = (w + 1u < (uint32_t)S::CLW) ? w + 1u : w;
+          const uint32_t lo = m.ld(S::CLOG + w), hi = m.ld(S::CLOG + w1);
+          const unsigned long long v = ((unsigned long long)hi << 32) | lo;
+          old = (uint32_t)(v >> sh) & 0x3FFFu;
+          const unsigned long long nv = app ? (v & ~(0x3FFFull << sh)) | ((unsigned long long)val << sh) : v;
+          m.st(S::CLOG + w1, (uint32_t)(nv >> 32));
+          m.st(S::CLOG + w, (uint32_t)nv);
+        } else {
+          const uint32_t cw = S::CLOG + (li >> 1), ch = li & 1u;
+          old = m.ld16h(cw, ch);
+          m.st16h(cw, ch, app ? val : old);
+        }
         lflags |= (trk & seen & (old != val)) ? (uint32_t)PXB_F_LOG_DIVERGENCE : 0u;
         lflags |= trk ? 0u : (uint32_t)PXB_F_LOG_TRUNC;
-        const bool app = trk & !seen;
-        m.st16h(cw, ch, app ? val : old);
         clog_len += app ? 1u : 0u;
       } else {
         if (log_len < clog_len) {
@@ -1392,13 +1411,15 @@ __host__ inline int layout_for(const pxb_config* c) {
   return 0;
 }
 __host__ inline int layout_wheel(int layout) {
-  return (layout == 1 || layout == 8) ? 16 : (layout == 3 || layout == 6 || layout == 7) ? 4 : 8;
+  return (layout == 1 || layout == 8) ? 16 : (layout == 3 || layout == 6 || layout == 7 || layout == 9) ? 4 : 8;
 }
 __host__ inline bool layout_compact(int layout) { return layout == 2 || layout == 3 || layout == 6 || layout == 7; }
 __host__ inline bool layout_simple(int layout) { return layout == 6 || layout == 7; }
 // (8: layout 4 on the 16-step wheel with its topology's larger pool, the
 // second stage of two-stage log mode, pxb_run_device)
-__host__ inline bool layout_log(int layout) { return layout == 4 || layout == 8; }
+// (9: layout 4 slimmed -- byte reply seqs in registers -- on the 4-step wheel,
+// for log mode with delays <= 4 over <= 10 links: the first stage there)
+__host__ inline bool layout_log(int layout) { return layout == 4 || layout == 8 || layout == 9; }
 
 }  // namespace ev
 }  // namespace pxb

@@ -33,6 +33,7 @@ PXB_EV_FOR_N(4, true, false, false, 2)         // tight simple schedule (layout 
 PXB_EV_FOR_N(8, false, true, false, false)     // log mode
 PXB_EV_FOR_N(16, false, true, false, false)    // log mode, second stage (layout 8: 16-step wheel, larger pool)
 PXB_EV_FOR_N(8, false, false, true, false)     // slim
+PXB_EV_FOR_N(4, false, true, true, false)      // log mode, slim, 4-step wheel (layout 9)
 #endif
 }  // namespace ev
 }  // namespace pxb

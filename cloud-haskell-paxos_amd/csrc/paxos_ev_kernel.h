@@ -106,6 +106,11 @@ struct EvKParams {
 #ifndef PXB_EV_LG_POOL
 #define PXB_EV_LG_POOL 19
 #endif
+// (slim log mode on the 4-step wheel, layout 9: see pxb_run_device; a 17-word
+// pool, 74 words, handed 5.5 instances per million on and measured slower)
+#ifndef PXB_EV_LGS_POOL
+#define PXB_EV_LGS_POOL 19
+#endif
 #ifndef PXB_EV_TIGHT_POOL
 #define PXB_EV_TIGHT_POOL 21
 #endif
@@ -114,7 +119,8 @@ struct EvKParams {
 template <int PM, int N, bool CMP, bool LG = false, bool SL = false, int SP = 0, int W = 8>
 struct EvPool {
   static constexpr int value = (SP == 2)             ? PXB_EV_TIGHT_POOL
-                               : (LG && PM * N <= 10 && W == 8) ? PXB_EV_LG_POOL
+                               : (LG && SL && W == 4 && PM * N <= 10) ? PXB_EV_LGS_POOL
+                               : (LG && PM * N <= 10 && W <= 8) ? PXB_EV_LG_POOL
                                : (CMP && PM * N <= 10) ? 16
                                : (PM * N <= 16)      ? (CMP ? PXB_EV_CMP_POOL : 32)
                                : CMP                ? PXB_EV_CMPW_POOL

@@ -175,7 +175,8 @@ extern "C" int ev_host_run(const pxb_config* cfg, pxb_result* out, uint32_t* dig
   if (layout == 2 && cfg->delay_max > 8) return -1;
   if ((layout == 3 || layout == 6 || layout == 7) && cfg->delay_max > 4) return -1;
   if ((layout == 6 || layout == 7) && (cfg->loss_ppm || cfg->skew_max || (cfg->flags & PXB_CFG_RANDOMIZE) || cfg->n_ticks > 1)) return -1;
-  if ((layout == 4 || layout == 8) != (cfg->n_ticks > 1)) return -1;   // log mode runs on the log-mode fields only
+  if ((layout == 4 || layout == 8 || layout == 9) != (cfg->n_ticks > 1)) return -1;   // log mode runs on the log-mode fields only
+  if (layout == 9 && cfg->delay_max > 4) return -1;
   if ((layout == 0 || layout == 5) && cfg->delay_max > 8) return -1;
   // tests: the shape's proposer capacity; below n_proposers (fuzzed batches
   // only) it is the split routing of pxb_run_device, whose instances with more
@@ -196,6 +197,7 @@ extern "C" int ev_host_run(const pxb_config* cfg, pxb_result* out, uint32_t* dig
     case 6: return run_w<4, true, false, false, 1>(cfg, pm, out, dig, acc, totals, bail_ids, n_bail, micro_steps);
     case 7: return run_w<4, true, false, false, 2>(cfg, pm, out, dig, acc, totals, bail_ids, n_bail, micro_steps);
     case 8: return run_w<16, false, true>(cfg, pm, out, dig, acc, totals, bail_ids, n_bail, micro_steps);
+    case 9: return run_w<4, false, true, true>(cfg, pm, out, dig, acc, totals, bail_ids, n_bail, micro_steps);
   }
   return -1;
 }

@@ -275,6 +275,26 @@ def test_log_mode_second_stage_layout(P, N, loss, delay, ticks, period, crash, m
     assert cnt["executes"] >= cnt["decided"] and len(bails) == 0
 
 
+@pytest.mark.parametrize("P,N,loss,delay,ticks,period,crash", [
+    (2, 5, 100000, 4, 16, 8, 200000),    # faulty log mode (BASELINE-like, extra.log_mode_faulty)
+    (1, 9, 300000, 4, 10, 3, 300000),
+    (3, 3, 200000, 3, 12, 5, 100000),
+    (2, 2, 0, 1, 16, 8, 0),
+    (2, 4, 0, 4, 16, 2, 0),              # responses pile up
+    (1, 5, 10000, 2, 100, 8, 150000)])   # logs past LOG_TRACK: every packed canonical-log position
+def test_log_mode_slim_4step_layout(P, N, loss, delay, ticks, period, crash, monkeypatch):
+    """Layout 9: the log-mode shape with byte reply seqs in registers, on the
+    4-step wheel, its canonical log packed (14 words), a 19-word pool (75 LDS
+    words, 8 waves per CU): the first stage of log mode with delays <= 4 over
+    <= 10 links.  Exact against the oracle, its hand-offs rare."""
+    monkeypatch.setenv("EV_LAYOUT", "9")
+    cfg = pxb.Config(seed=0x1C9 + 16 * P + N, n_proposers=P, n_acceptors=N, loss_ppm=loss,
+                     delay_max=delay, skew_max=3, crash_ppm=crash, crash_len_max=12,
+                     crash_start_max=30, step_cap=1024, n_ticks=ticks, tick_period=period)
+    _, cnt, bails = check(cfg, 91, 1500, max_bail_frac=0.01)
+    assert cnt["executes"] >= cnt["decided"]
+
+
 @pytest.mark.parametrize("P,loss,crash,period,delay,clen",[(1, 10000, 150000, 8, 2, 20), (2, 0, 100000, 12, 1, 30)])
 def test_log_mode_past_log_track(P, loss, crash, period, delay, clen):
     """100 Ticks per proposer: logs past LOG_TRACK = 32 set LOG_TRUNC; the
@@ -308,18 +328,18 @@ def test_random_log_mode_schedules(i):
 # fill it to within ~1 KiB measured no gain ("LDS to spare"; LDS
 # is allocated in 1 KiB steps per block), so every shape keeps >= 4 KiB free at
 # its residency (round 5: the tight layout's 12 x 13 KiB, measured resident).
-@pytest.mark.parametrize("c,pm,words,blocks", [
-    (4, 2, 60, 10),      # compact, 4-step wheel (layout 6: the tight routing's second launch)
-    (-4, 2, 50, 12),     # tight (layout 7: halfword response FIFOs, 21-word pool)
-    (3, 2, 44, 12),      # compact, 16-word pool (12 = the VGPR limit)
-    (5, 3, 120, 5),      # slim, P = 3 share
-    (5, 2, 75, 8),       # slim, P <= 2 share (halfword response links, 28-word pool)
-    (7, 2, 86, 7),       # faulty log mode (19-word pool)
+@pytest.mark.parametrize("c,pm,layout,words,blocks", [
+    (4, 2, None, 60, 10),   # compact, 4-step wheel (layout 6: the tight routing's second launch)
+    (4, 2, "7", 50, 12),    # tight (layout 7: halfword response FIFOs, 21-word pool)
+    (3, 2, None, 44, 12),   # compact, 16-word pool (12 = the VGPR limit)
+    (5, 3, None, 120, 5),   # slim, P = 3 share
+    (5, 2, None, 75, 8),    # slim, P <= 2 share (halfword response links, 28-word pool)
+    (7, 2, None, 86, 7),    # faulty log mode (layout 4, 19-word pool: delays above 4)
+    (7, 2, "9", 75, 8),     # faulty log mode's first stage (layout 9: byte reply seqs, 4-step wheel, packed log)
 ])
-def test_layout_words_leave_lds_to_spare(c, pm, words, blocks, monkeypatch):
-    if c < 0:
-        c = -c
-        monkeypatch.setenv("EV_LAYOUT", "7")
+def test_layout_words_leave_lds_to_spare(c, pm, layout, words, blocks, monkeypatch):
+    if layout:
+        monkeypatch.setenv("EV_LAYOUT", layout)
     cfg = pxb.CONFIGS[c]
     if pm != cfg.n_proposers:
         monkeypatch.setenv("EV_PM", str(pm))

@@ -143,6 +143,23 @@ def test_log_mode_sanitized(exe, P, N, loss, delay, ticks, period, crash):
     check(exe, cfg, 321, 300)
 
 
+@pytest.mark.parametrize("layout", ["8", "9"])
+@pytest.mark.parametrize("P,N,loss,delay,ticks,period,crash", [
+    (2, 5, 100000, 4, 16, 8, 200000),       # faulty log mode (bench extra.log_mode_faulty)
+    (1, 5, 10000, 2, 100, 8, 150000),       # logs past LOG_TRACK: every packed canonical-log position
+    (2, 5, 0, 4, 16, 2, 0),                 # responses pile up (the sanitized build has N = 2, 5, 7, 9)
+])
+def test_log_mode_stages_sanitized(exe, layout, P, N, loss, delay, ticks, period, crash):
+    """The two-stage log mode's shapes: layout 9 (first stage, delays <= 4:
+    byte reply seqs, 4-step wheel, the canonical log's 14-bit commands packed
+    across words) and layout 8 (second stage: 16-step wheel, 32-word pool),
+    with every word and halfword index checked."""
+    cfg = pxb.Config(seed=0x1D61 + 16 * P + N, n_proposers=P, n_acceptors=N, loss_ppm=loss, delay_max=delay,
+                     skew_max=3, crash_ppm=crash, crash_len_max=12, crash_start_max=30,
+                     step_cap=2048 if ticks > 50 else 1024, n_ticks=ticks, tick_period=period)
+    check(exe, cfg, 55, 300, {"EV_LAYOUT": layout}, max_bail_frac=0.05)
+
+
 @pytest.mark.parametrize("i", range(8))
 def test_random_schedules_sanitized(exe, i):
     rng = np.random.default_rng(0x5A71 + i)

@@ -989,11 +989,33 @@ def test_log_mode_two_stage_routing(gpu_lib):
     h1, h2 = pxb.handoff_counts(0, reset=True)
     assert h1 >= 20 and h2 <= h1 // 4, (h1, h2)
     a = pxb.run(cfg, first, n, want_acceptors=True)
-    for env in ({"PXB_NO_LG2": "1"}, {"PXB_EV_BAIL_CAP": "0"}, {"PXB_EV_BAIL_CAP": "3"}):
+    for env in ({"PXB_NO_LG2": "1"}, {"PXB_EV_BAIL_CAP": "0"}, {"PXB_EV_BAIL_CAP": "3"}, {"PXB_NO_LGS": "1"},
+                {"PXB_NO_LGS": "1", "PXB_NO_LG2": "1"}):
         b = _with_env(env, lambda: pxb.run(cfg, first, n, want_acceptors=True))
         for x, y in zip(a[:3], b[:3]):
             assert np.array_equal(x, y), env
         assert a[3] == b[3], env
+
+
+def test_log_mode_first_stage_layouts(gpu_lib):
+    """Faulty log mode with delays <= 4 over <= 10 links runs its first stage on
+    layout 9 (byte reply seqs, 4-step wheel, packed canonical log: 8 waves per
+    CU), with longer delays on layout 4: both against the oracle, and layout 9
+    against layout 4 (PXB_NO_LGS=1) on the bench's batch, logs past LOG_TRACK
+    included."""
+    for cfg in (pxb.LOG_FAULTY_CONFIG,
+                pxb.Config(seed=0x7A0D, n_proposers=1, n_acceptors=5, loss_ppm=10000, delay_max=2, skew_max=2,
+                           crash_ppm=150000, crash_len_max=20, crash_start_max=400, step_cap=2048, n_ticks=100,
+                           tick_period=8),
+                pxb.Config(seed=0x7A0E, n_proposers=2, n_acceptors=5, loss_ppm=100000, delay_max=6, skew_max=3,
+                           crash_ppm=200000, crash_len_max=16, crash_start_max=64, step_cap=1024, n_ticks=16,
+                           tick_period=8)):
+        _cmp(cfg, 777, 6000)
+        a = pxb.run(cfg, 1 << 37, 30000, want_acceptors=True)
+        b = _with_env({"PXB_NO_LGS": "1"}, lambda: pxb.run(cfg, 1 << 37, 30000, want_acceptors=True))
+        for x, y in zip(a[:3], b[:3]):
+            assert np.array_equal(x, y)
+        assert a[3] == b[3]
 
 
 def test_log_mode_contiguous_faulty_config(gpu_lib):

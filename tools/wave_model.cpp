@@ -185,7 +185,14 @@ int main(int argc, char** argv) {
     cfg.delay_max = 4; cfg.skew_max = 3; cfg.crash_ppm = 200000; cfg.crash_len_max = 16;
     cfg.crash_start_max = 64; cfg.step_cap = 1024; cfg.n_ticks = 16; cfg.tick_period = 8;
     std::vector<uint32_t> bailed;
-    model<2, 5, 8, false, true, false>(&cfg, n, rmin, nullptr, &bailed);
+    // (LGW=4: the log-mode shape slimmed -- byte reply seqs in registers -- on the
+    // 4-step wheel, for delays <= 4; LGW=8: the same on the 8-step wheel)
+    if (getenv("LGW")) {
+      if (atoi(getenv("LGW")) == 4) model<2, 5, 4, false, true, true>(&cfg, n, rmin, nullptr, &bailed);
+      else model<2, 5, 8, false, true, true>(&cfg, n, rmin, nullptr, &bailed);
+    } else {
+      model<2, 5, 8, false, true, false>(&cfg, n, rmin, nullptr, &bailed);
+    }
     if (getenv("STAGE2")) {   // the LG shape on the 16-step wheel (its larger pool) over the hand-offs
       printf("-- second stage over %zu hand-offs\n", bailed.size());
       std::vector<uint32_t> b2;
