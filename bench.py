@@ -98,6 +98,24 @@ def scaling_of(c: int) -> str:
     return "strong" if c in (4, 5) else "weak"
 
 
+_STREAM_POOL = []
+
+
+def step_streams(stream, dev, ns):
+    """The first ns step streams: the main stream, then streams created once per
+    process and shared by every workload.  (A process gets GPU_MAX_HW_QUEUES = 4
+    hardware queues, which its streams share round-robin in creation order: a
+    workload that made streams of its own after the earlier ones' could land two
+    of its step streams on one queue, where they run one after the other.)"""
+    import torch
+    if not _STREAM_POOL:
+        _STREAM_POOL.append(stream)
+    while len(_STREAM_POOL) < ns:
+        _STREAM_POOL.append(torch.cuda.Stream(dev))
+    assert _STREAM_POOL[0] is stream
+    return _STREAM_POOL[:ns]
+
+
 class GpuLeg:
     """The measured work of one rank: pxb_run_device over fresh instance ids,
     asynchronous, timed with an event pair.  Steps of up to 2^24 instances
@@ -116,14 +134,14 @@ class GpuLeg:
     size: 2^28 per step, 4.3 ms with two against 5.4 ms alone.  All K steps complete
     inside the timed region either way."""
 
-    def __init__(self, cfg, n, rank, world, stream, dev, outputs=True):
+    def __init__(self, cfg, n, rank, world, stream, dev, outputs=True, streams=0):
         import torch
         import pxb
         self.torch, self.pxb = torch, pxb
         self.cfg, self.n, self.rank, self.world, self.stream, self.dev = cfg, n, rank, world, stream, dev
         fault_free = cfg.loss_ppm == 0 and cfg.crash_ppm == 0      # (the fault-free kernels: not persistent)
-        ns = STEP_STREAMS or (2 if (n <= (1 << 24) or fault_free) else 1)
-        self.streams = [stream] + [torch.cuda.Stream(dev) for _ in range(ns - 1)]
+        ns = streams or STEP_STREAMS or (2 if (n <= (1 << 24) or fault_free) else 1)
+        self.streams = step_streams(stream, dev, ns)
         ns = len(self.streams)
         # (outputs=False: run totals only, no per-instance records)
         self.out = [torch.empty((n, 4), dtype=torch.int32, device=dev) if outputs else None for _ in range(ns)]
@@ -403,6 +421,7 @@ def faulty_line(name, c, n, steps, warmup, stream, dev, warm_n, rank=0, world=1,
 
 
 LOG_STEPS = 8                # timed steps of the faulty-log-mode lines (round 5: 2)
+LOG_STREAMS = 3              # their step streams (MI355X, 8 steps: 2^22 23.3 -> 23.0 ms, 2^20 7.2 -> 6.85 ms vs 2)
 
 
 def log_faulty_line(stream, dev, n=1 << 22, general=True):
@@ -420,16 +439,17 @@ def log_faulty_line(stream, dev, n=1 << 22, general=True):
     more there (the 2-step rate is reported beside it)."""
     import pxb
     cfg = pxb.LOG_FAULTY_CONFIG
-    es, ek, ecnt = run_workload(GpuLeg(cfg, n, 0, 1, stream, dev), n, LOG_STEPS, 1, 1)
+    es, ek, ecnt = run_workload(GpuLeg(cfg, n, 0, 1, stream, dev, streams=LOG_STREAMS), n, LOG_STEPS, 1, 1)
     e2s, _, e2cnt = run_workload(GpuLeg(cfg, n, 0, 1, stream, dev), n, 2, 1, 1)
     line = {"workload": "faulty log mode: P=2, N=5, 10% loss, delay [1,4], crash windows, 16 Ticks / 8 steps",
-            "instances_per_step": n, "steps": LOG_STEPS, "instances_per_s": ecnt["instances"] / es,
+            "instances_per_step": n, "steps": LOG_STEPS, "step_streams": LOG_STREAMS,
+            "instances_per_s": ecnt["instances"] / es,
             "commands_committed_per_s": ecnt["executes"] / es, "kernel_ms": ek,
-            "instances_per_s_2_steps": e2cnt["instances"] / e2s,
+            "instances_per_s_2_steps": e2cnt["instances"] / e2s,     # (2 steps on 2 streams: round 5's measurement)
             "roofline": roofline("config7", n, ek, ecnt["canon_bytes"] / LOG_STEPS), "counters": ecnt}
     if general:
         with pxb.hooks(PXB_NO_EV="1"):
-            gs, gk, gcnt = run_workload(GpuLeg(cfg, n, 0, 1, stream, dev), n, LOG_STEPS, 1, 1)
+            gs, gk, gcnt = run_workload(GpuLeg(cfg, n, 0, 1, stream, dev, streams=LOG_STREAMS), n, LOG_STEPS, 1, 1)
         assert gcnt == ecnt, (gcnt, ecnt)
         line["general_kernel"] = {"instances_per_s": gcnt["instances"] / gs, "kernel_ms": gk}
         line["speedup_vs_general_kernel"] = gk / ek
