@@ -32,6 +32,11 @@ module PaxosBatch
   , shutdown
   , withEngine
   , handoffCounts
+    -- * Per-instance trace (the reference's `say` dumps, Server.hs:85, Client.hs:108)
+  , AcceptorState (..)
+  , ProposerState (..)
+  , TraceStep (..)
+  , traceInstance
   ) where
 
 import           Common                (Command, Proposal, Ticket (..))
@@ -141,6 +146,8 @@ foreign import ccall safe "pxb_shutdown"
   c_pxb_shutdown :: IO CInt
 foreign import ccall safe "pxb_handoff_counts"
   c_pxb_handoff_counts :: CInt -> Ptr Word64 -> CInt -> IO CInt
+foreign import ccall safe "pxb_trace_instance"
+  c_pxb_trace_instance :: Ptr BatchConfig -> Word64 -> Ptr Word32 -> Word32 -> Ptr Word32 -> Ptr Word32 -> IO CInt
 
 -- | The ABI this module was written against (include/paxos_batch.h).
 expectedAbi :: Int
@@ -232,3 +239,69 @@ decode v t r f = Outcome
   , oSteps   = fromIntegral (f `shiftR` 16)
   , oFlags   = [fl | fl <- [minBound .. maxBound], testBit f (fromEnum fl)]
   }
+
+-- | An acceptor at the end of a traced step (ServerState, Server.hs:24-31).
+data AcceptorState = AcceptorState
+  { asLargestTicket :: Ticket
+  , asProposal      :: Maybe Proposal
+  , asLogLength     :: !Int
+  , asDead          :: !Bool         -- ^ after a Server.hs:76 panic (Q6)
+  , asLogDigest     :: !Word32       -- ^ FNV-1a of its log so far (docs/SEMANTICS.md §7)
+  } deriving (Show)
+
+-- | A proposer at the end of a traced step (ClientState, Client.hs:58-67).
+data ProposerState = ProposerState
+  { psTicket     :: Ticket
+  , psCommand    :: Maybe Command    -- ^ _mCommand
+  , psAcks       :: !Int
+  , psPhase      :: !Int             -- ^ 0 Idle, 1 Round1, 2 Round2
+  , psMostRecent :: Maybe Proposal   -- ^ Round1: MostRecent
+  , psRound2     :: Maybe Command    -- ^ Round2: the proposed command
+  , psPending    :: !Bool            -- ^ Round2: _originalCommandPending
+  } deriving (Show)
+
+-- | One record of 'traceInstance': the state after a step (steps with nothing
+-- due and no Tick change nothing and are skipped).  'tsInFlight' is Nothing
+-- when copies of a broadcast were still to be sent (production variant only).
+data TraceStep = TraceStep
+  { tsStep      :: !Int
+  , tsInFlight  :: Maybe Int
+  , tsAcceptors :: [AcceptorState]
+  , tsProposers :: [ProposerState]
+  } deriving (Show)
+
+-- | pxb_trace_instance: instance @i@ of @cfg@ (single decree or, ABI 5, log
+-- mode) on one GPU lane, its state recorded at the end of every step, at most
+-- @maxRecords@ records; with its outcome.  What 'runBatch' cannot show: where
+-- a run departs from the reference's schedule, step by step.
+traceInstance :: BatchConfig -> Word64 -> Int -> IO (Either String ([TraceStep], Outcome))
+traceInstance cfg i maxRecords = do
+  let nw = 73                                      -- sizeof(pxb_trace_step) / 4
+  buf <- mallocForeignPtrArray (nw * maxRecords)
+  with cfg { bcFirst = i, bcCount = 1 } $ \pc ->
+    withForeignPtr buf $ \pb ->
+      allocaArray 1 $ \pn ->
+        allocaArray 4 $ \pres -> do
+          rc <- c_pxb_trace_instance pc i pb (fromIntegral maxRecords) pn pres
+          if rc /= 0
+            then Left <$> (c_pxb_strerror rc >>= peekCString)
+            else do
+              [n] <- peekArray 1 pn
+              recs <- forM [0 .. fromIntegral n - 1] $ \k -> step <$> peekArray nw (advancePtr pb (nw * k))
+              [v, t, r, f] <- peekArray 4 pres
+              pure (Right (recs, decode v t r f))
+  where
+    step w =
+      let at k = w !! k
+          nA = fromIntegral (at 2); nP = fromIntegral (at 3)
+          cmd c = if c == 0 then Nothing else Just (commandOf c)
+          prop t c = if c == 0 then Nothing else Just (Ticket (fromIntegral (fromIntegral t :: Int32)), commandOf c)
+          acc a = let b = 4 + 4 * a; meta = at (b + 3)
+                  in AcceptorState (Ticket (fromIntegral (fromIntegral (at b) :: Int32))) (prop (at (b + 1)) (at (b + 2)))
+                                   (fromIntegral (meta .&. 0x7FFFFFFF)) (testBit meta 31) (at (40 + a))
+          pro q = let b = 49 + 8 * q
+                  in ProposerState (Ticket (fromIntegral (fromIntegral (at b) :: Int32))) (cmd (at (b + 1)))
+                                   (fromIntegral (at (b + 2))) (fromIntegral (at (b + 3))) (prop (at (b + 4)) (at (b + 5)))
+                                   (cmd (at (b + 6))) (at (b + 7) /= 0)
+      in TraceStep (fromIntegral (at 0)) (if at 1 == 0xFFFFFFFF then Nothing else Just (fromIntegral (at 1)))
+                   (map acc [0 .. nA - 1]) (map pro [0 .. nP - 1])
