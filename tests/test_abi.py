@@ -202,3 +202,25 @@ def test_wire_device_entry_points_check_their_buffers():
             return 64
     with pytest.raises(ValueError, match="uint8"):
         pxb._check_bytes("d_bytes", _PosingAsDevice(), 1)
+
+def test_trace_record_layout_matches_bindings():
+    """pxb_trace_step as the Python mirror (pxb.TRACE_WORDS, word offsets in
+    trace_instance) and the Haskell binding (PaxosBatch.traceInstance: 73
+    words, digests from word 40, proposers from word 49, 8 words each) read it."""
+    src = r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "paxos_batch.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu\n", sizeof(pxb_trace_step), offsetof(pxb_trace_step, acc),
+         offsetof(pxb_trace_step, log_digest), offsetof(pxb_trace_step, prop), sizeof(pxb_trace_prop));
+  return 0;
+}'''
+    tmp = "/tmp/pxb_trace_layout"
+    with open(tmp + ".c", "w") as f:
+        f.write(src)
+    subprocess.run(["gcc", "-I", os.path.dirname(HEADER), "-o", tmp, tmp + ".c"], check=True)
+    size, acc, dig, prop, psize = (int(x) for x in subprocess.run([tmp], capture_output=True, text=True).stdout.split())
+    assert (size, acc, dig, prop, psize) == (4 * pxb.TRACE_WORDS, 16, 160, 196, 32)
+    hs = open(os.path.join(os.path.dirname(HEADER), "..", "cloud-haskell-paxos_amd", "hs", "PaxosBatch.hs")).read()
+    assert "let nw = 73" in hs and "at (40 + a)" in hs and "let b = 49 + 8 * q" in hs and "let b = 4 + 4 * a" in hs
