@@ -116,9 +116,13 @@ struct EvKParams {
 #endif
 // (W: the log-mode shape on the 16-step wheel, the second stage behind the
 // 8-step one, takes the larger pool of its topology)
+#ifndef PXB_EV_SLW4_POOL
+#define PXB_EV_SLW4_POOL 32
+#endif
 template <int PM, int N, bool CMP, bool LG = false, bool SL = false, int SP = 0, int W = 8>
 struct EvPool {
   static constexpr int value = (SP == 2)             ? PXB_EV_TIGHT_POOL
+                               : (SL && !LG && W == 4 && PM * N > 18) ? PXB_EV_SLW4_POOL
                                : (LG && SL && W == 4 && PM * N <= 10) ? PXB_EV_LGS_POOL
                                : (LG && PM * N <= 10 && W <= 8) ? PXB_EV_LG_POOL
                                : (CMP && PM * N <= 10) ? 16

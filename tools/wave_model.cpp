@@ -166,6 +166,21 @@ int main(int argc, char** argv) {
     if (getenv("C5W4")) {   // (its delay_max <= 4 instances on the compact 4-step wheel)
       cfg.delay_max = 4;
       model<3, 9, 4, true, false, false>(&cfg, n, rmin);
+    } else if (getenv("C5SW4")) {
+      // the slim P = 3 shape on the 4-step wheel over the P = 3, delay <= 4
+      // instances among the first n (a first stage in front of layout 5's)
+      const EvParams p = make_params(&cfg);
+      using Probe = EvLane<3, 9, 44, 8, false, HostMem, true, false, true, 0>;
+      std::vector<uint32_t> mem(256), ids, bailed;
+      Probe q;
+      q.m = HostMem{mem.data()};
+      q.set_keys(p);
+      for (uint32_t g = 0; g < n; ++g) {
+        q.init(p, g);
+        if (q.P == 3u && q.dmax <= 4u) ids.push_back(g);
+      }
+      printf("-- slim W4 over %zu P = 3, delay <= 4 instances of %u\n", ids.size(), n);
+      model<3, 9, 4, false, false, true>(&cfg, 0, rmin, &ids, &bailed);
     } else {
       std::vector<uint32_t> bailed;
       model<3, 9, 8, false, false, true>(&cfg, n, rmin, nullptr, &bailed);
