@@ -117,7 +117,7 @@ struct EvKParams {
 // (W: the log-mode shape on the 16-step wheel, the second stage behind the
 // 8-step one, takes the larger pool of its topology)
 #ifndef PXB_EV_SLW4_POOL
-#define PXB_EV_SLW4_POOL 32
+#define PXB_EV_SLW4_POOL 31
 #endif
 template <int PM, int N, bool CMP, bool LG = false, bool SL = false, int SP = 0, int W = 8>
 struct EvPool {
