@@ -8,7 +8,11 @@ three-proposer split (fuzzed P), faulty log mode, and the general kernel
 beyond them.  Every batch is compared with the C oracle instance by instance
 (results, digests) and in its run totals.
 
-    python tests/fuzz_gpu.py [n_configs] [instances_per_config] [seed]
+    python tests/fuzz_gpu.py [n_configs] [instances_per_config] [seed] [kinds]
+
+kinds: a comma list to cycle through (default simple,simple,compact,split,log,any,
+the rounds 4-6 runs; p3 adds three-proposer schedules that are not fuzzed per
+instance).
 """
 import os
 import sys
@@ -40,6 +44,10 @@ def draw(rng, kind):
         common.update(n_proposers=3, n_acceptors=int(rng.integers(5, 10)))
         return pxb.Config(loss_ppm=int(rng.integers(0, 400000)), delay_max=int(rng.integers(1, 9)),
                           skew_max=int(rng.integers(0, 4)), randomize=True, **common)
+    if kind == "p3":                  # three proposers on every instance (not fuzzed): slim / compact / general
+        common.update(n_proposers=3)
+        return pxb.Config(loss_ppm=int(rng.integers(0, 400000)), delay_max=int(rng.integers(1, 9)),
+                          skew_max=int(rng.integers(0, 4)), **common)
     if kind == "log":                 # faulty log mode (the per-lane LG shape, delays <= 8)
         return pxb.Config(loss_ppm=int(rng.integers(0, 200000)), delay_max=int(rng.integers(1, 9)),
                           skew_max=int(rng.integers(0, 4)), n_ticks=int(rng.integers(2, 12)),
@@ -52,7 +60,7 @@ def main():
     n_cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 200
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
     rng = np.random.default_rng(int(sys.argv[3]) if len(sys.argv) > 3 else 0xF022)
-    kinds = ["simple", "simple", "compact", "split", "log", "any"]
+    kinds = sys.argv[4].split(",") if len(sys.argv) > 4 else ["simple", "simple", "compact", "split", "log", "any"]
     t0 = time.time()
     bad = 0
     for i in range(n_cfg):

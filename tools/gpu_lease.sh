@@ -8,7 +8,7 @@
 # steps (arguments after ':' separated by ','):
 #   tests                      the full -m gpu suite
 #   tests:<pytest -k expr>     a subset of it
-#   fuzz:<schedules>,<n>[,<seed>]   tests/fuzz_gpu.py, GPU vs the C oracle
+#   fuzz:<schedules>,<n>[,<seed>[,<kind>+<kind>...]]   tests/fuzz_gpu.py, GPU vs the C oracle
 #   bench                      the default bench line (bench.py, CPU baseline and extra included)
 #   bench:<bench.py args>      e.g. bench:--no-cpu --no-extra --steps 5  (spaces allowed)
 #   ab:<lib.so>+<lib.so>...    tools/ab_ev.py A/B of library variants (AB_CASES, AB_PASSES from the env)
@@ -38,8 +38,8 @@ for step in "$@"; do
       fi
       rc=$?; tail -3 $O/pytest_$k.log; [ $rc -eq 0 ] || { tail -40 $O/pytest_$k.log; exit 1; } ;;
     fuzz)
-      IFS=, read -r ns ni seed <<< "$arg"
-      timeout -k 10 600 python3 -u tests/fuzz_gpu.py $ns $ni $seed > $O/fuzz_$k.txt 2>&1 || { tail -20 $O/fuzz_$k.txt; exit 1; }
+      IFS=, read -r ns ni seed kinds <<< "$arg"
+      timeout -k 10 600 python3 -u tests/fuzz_gpu.py $ns $ni $seed ${kinds//+/,} > $O/fuzz_$k.txt 2>&1 || { tail -20 $O/fuzz_$k.txt; exit 1; }
       tail -1 $O/fuzz_$k.txt ;;
     bench)
       timeout -k 10 600 python3 -u bench.py $arg > $O/bench_$k.json 2> $O/bench_$k.err || { tail -20 $O/bench_$k.err; exit 1; }
