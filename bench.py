@@ -35,6 +35,15 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "cloud-haskell-paxos_amd"))
 
+# HIP hardware queues per process (HIP's default, and the GPU box's setting: 4).
+# The faulty-log-mode lines keep LOG_STREAMS calls in flight, one step stream
+# each, and streams beyond the queue count share a queue, where they run one
+# after the other; workloads on one stream are unaffected.  Raised before
+# anything initialises HIP (torch is imported lazily), never lowered.
+HW_QUEUES = 16
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < HW_QUEUES:
+    os.environ["GPU_MAX_HW_QUEUES"] = str(HW_QUEUES)
+
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
 # VALU issue peak: 256 CUs x 4 SIMDs, a wave64 VALU instruction every 2 cycles
 # per SIMD (MI355X_MICROARCH.md, "Wave scheduling") = 2 wave-instructions per
@@ -103,10 +112,11 @@ _STREAM_POOL = []
 
 def step_streams(stream, dev, ns):
     """The first ns step streams: the main stream, then streams created once per
-    process and shared by every workload.  (A process gets GPU_MAX_HW_QUEUES = 4
+    process and shared by every workload.  (A process gets GPU_MAX_HW_QUEUES
     hardware queues, which its streams share round-robin in creation order: a
     workload that made streams of its own after the earlier ones' could land two
-    of its step streams on one queue, where they run one after the other.)"""
+    of its step streams on one queue, where they run one after the other; main()
+    creates them all first.)"""
     import torch
     if not _STREAM_POOL:
         _STREAM_POOL.append(stream)
@@ -421,7 +431,9 @@ def faulty_line(name, c, n, steps, warmup, stream, dev, warm_n, rank=0, world=1,
 
 
 LOG_STEPS = 8                # timed steps of the faulty-log-mode lines (round 5: 2)
-LOG_STREAMS = 3              # their step streams (MI355X, 8 steps: 2^22 23.3 -> 23.0 ms, 2^20 7.2 -> 6.85 ms vs 2)
+LOG_STREAMS = 8              # their step streams: every call in flight on its own stream and hardware queue
+# (MI355X, 8 steps, profiles/r06_notes/ab_log_streams.txt: 2^20 144 / 153 / 161 / 162-171 M/s
+# on 2 / 3 / 4 / 8 streams, 2^22 180 / 183 / 186 / 188-191; 8 streams need the 8 queues above)
 
 
 def log_faulty_line(stream, dev, n=1 << 22, general=True):
@@ -429,20 +441,21 @@ def log_faulty_line(stream, dev, n=1 << 22, general=True):
     to 4, crash windows, 16 Ticks 8 steps apart) on the per-lane kernel's
     log-mode shape, and (general=True) the same batch on the general kernel
     (PXB_NO_EV=1) for the speed-up; the totals of the two must be identical.
-    LOG_STEPS timed steps on the two step streams.  The batch's instance
+    LOG_STEPS timed steps on LOG_STREAMS step streams.  The batch's instance
     lengths have a heavy tail (median 124 steps, the longest ~950: 7.7 x), so
     a call's last waves run its longest instances for 2-5 ms after its work
     queue drained (profiles/r06_notes/lg_wave_times_2p20.txt: at 2^20 the
-    queue drains at 5.0 ms and the last wave ends at 10.2 ms); consecutive
-    steps on two streams fill part of that tail, and one tail stays exposed
-    per measurement.  Round 5 timed 2 steps, so that exposed tail weighed 4x
-    more there (the 2-step rate is reported beside it)."""
+    queue drains at 5.0 ms and the last wave ends at 10.2 ms); the other calls
+    in flight on their own streams fill that tail, and one tail stays exposed
+    per measurement.  Round 5 timed 2 steps on 2 streams (that rate is
+    reported beside it)."""
     import pxb
     cfg = pxb.LOG_FAULTY_CONFIG
     es, ek, ecnt = run_workload(GpuLeg(cfg, n, 0, 1, stream, dev, streams=LOG_STREAMS), n, LOG_STEPS, 1, 1)
     e2s, _, e2cnt = run_workload(GpuLeg(cfg, n, 0, 1, stream, dev), n, 2, 1, 1)
     line = {"workload": "faulty log mode: P=2, N=5, 10% loss, delay [1,4], crash windows, 16 Ticks / 8 steps",
             "instances_per_step": n, "steps": LOG_STEPS, "step_streams": LOG_STREAMS,
+            "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
             "instances_per_s": ecnt["instances"] / es,
             "commands_committed_per_s": ecnt["executes"] / es, "kernel_ms": ek,
             "instances_per_s_2_steps": e2cnt["instances"] / e2s,     # (2 steps on 2 streams: round 5's measurement)
@@ -510,6 +523,9 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     stream = torch.cuda.Stream(dev)
+    # (every step stream a workload may take, created first: consecutive
+    # creations get distinct hardware queues, HW_QUEUES)
+    step_streams(stream, dev, max(LOG_STREAMS, 2))
     c = args.config
     cfg = pxb.CONFIGS[c]
     n = step_instances(c, args.instances, world)
