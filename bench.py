@@ -71,7 +71,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extra", action="store_true")
     ap.add_argument("--dry-run", action="store_true", help="CPU ranks (gloo), synthetic work: launcher test only")
-    ap.add_argument("--streams", type=int, default=0, help="step streams (default: 2 up to 2^24 instances per step, else 1)")
+    ap.add_argument("--streams", type=int, default=0, help="step streams (default: faulty steps of up to 2^24 instances 4, larger ones 1; fault-free 2)")
     ap.add_argument("--one-stream", action="store_true",
                     help="all steps on one stream (A/B of the two-stream step pipeline)")
     return ap.parse_args()
@@ -129,8 +129,10 @@ def step_streams(stream, dev, ns):
 class GpuLeg:
     """The measured work of one rank: pxb_run_device over fresh instance ids,
     asynchronous, timed with an event pair.  Steps of up to 2^24 instances
-    alternate between two HIP streams with their own output buffers (double
-    buffering): the per-lane kernel is persistent (its grid is the resident
+    rotate over four HIP streams (hardware queues: HW_QUEUES) with their own
+    output buffers (round 6, MI355X, 8 steps: config 3 at 2^24 341 -> 346 M/s,
+    config 4 at 2^23 67.8 -> 68.5 M/s against two; profiles/r06_notes/
+    ab_log_streams.txt): the per-lane kernel is persistent (its grid is the resident
     capacity), so step k + 1's waves are dispatched onto the CUs that step k's
     last waves free up -- its tail (the slowest instances of the last waves,
     then the general kernel over its bailed ones: 2.5 % + 1 % of a
@@ -139,9 +141,10 @@ class GpuLeg:
     (the general kernel co-runs with the next per-lane kernel at a fraction
     of its speed, and the 1-block finalize behind it waits for that kernel to
     end), MI355X A/B (profiles/r04_notes/wave_times.txt): 2^23 +1.9 %, 2^24
-    +0.4 %, 2^25 +-0, 2^26 -0.7 % for two streams.  Fault-free batches (config 2:
+    +0.4 %, 2^25 +-0, 2^26 -0.7 % for two streams (round 6, 16 queues: 2^26 +-0.5 %,
+    config 5 at 2^25 -10 % on 2 or 3).  Fault-free batches (config 2:
     the fault-free per-lane kernel, not persistent) keep two streams at any
-    size: 2^28 per step, 4.3 ms with two against 5.4 ms alone.  All K steps complete
+    size: 2^28 per step, 4.3 ms with two against 5.4 ms alone (4 streams: the same).  All K steps complete
     inside the timed region either way."""
 
     def __init__(self, cfg, n, rank, world, stream, dev, outputs=True, streams=0):
@@ -150,7 +153,7 @@ class GpuLeg:
         self.torch, self.pxb = torch, pxb
         self.cfg, self.n, self.rank, self.world, self.stream, self.dev = cfg, n, rank, world, stream, dev
         fault_free = cfg.loss_ppm == 0 and cfg.crash_ppm == 0      # (the fault-free kernels: not persistent)
-        ns = streams or STEP_STREAMS or (2 if (n <= (1 << 24) or fault_free) else 1)
+        ns = streams or STEP_STREAMS or (2 if fault_free else 4 if n <= (1 << 24) else 1)
         self.streams = step_streams(stream, dev, ns)
         ns = len(self.streams)
         # (outputs=False: run totals only, no per-instance records)
@@ -525,7 +528,7 @@ def main():
     stream = torch.cuda.Stream(dev)
     # (every step stream a workload may take, created first: consecutive
     # creations get distinct hardware queues, HW_QUEUES)
-    step_streams(stream, dev, max(LOG_STREAMS, 2))
+    step_streams(stream, dev, max(LOG_STREAMS, 4))
     c = args.config
     cfg = pxb.CONFIGS[c]
     n = step_instances(c, args.instances, world)
@@ -580,7 +583,7 @@ def main():
                                              "over 8 GPUs) on 1 GPU", 4, pxb.CONFIG_INSTANCES[4] // 8, 4, 1,
                                              stream, dev, 1 << 22)
         extra["config3"] = faulty_line("BASELINE config 3: 2^24 instances", 3, pxb.CONFIG_INSTANCES[3],
-                                       2, 1, stream, dev, 1 << 22)
+                                       4, 1, stream, dev, 1 << 22)
         extra["config5"] = faulty_line("BASELINE config 5: 2^25 instances (the per-GPU share of 2^28 "
                                        "over 8 GPUs)", 5, pxb.CONFIG_INSTANCES[5] // 8, 1, 1, stream, dev,
                                        1 << 22)
