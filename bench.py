@@ -434,6 +434,7 @@ def faulty_line(name, c, n, steps, warmup, stream, dev, warm_n, rank=0, world=1,
 
 
 LOG_STEPS = 8                # timed steps of the faulty-log-mode lines (round 5: 2)
+LOG_SAME_TOTAL = 8 << 22     # (the 2^20 line's second rate: as many instances as the 2^22 line's 8 steps)
 LOG_STREAMS = 8              # their step streams: every call in flight on its own stream and hardware queue
 # (MI355X, 8 steps, profiles/r06_notes/ab_log_streams.txt: 2^20 144 / 153 / 161 / 162-171 M/s
 # on 2 / 3 / 4 / 8 streams, 2^22 180 / 183 / 186 / 188-191; 8 streams need the 8 queues above)
@@ -463,6 +464,12 @@ def log_faulty_line(stream, dev, n=1 << 22, general=True):
             "commands_committed_per_s": ecnt["executes"] / es, "kernel_ms": ek,
             "instances_per_s_2_steps": e2cnt["instances"] / e2s,     # (2 steps on 2 streams: round 5's measurement)
             "roofline": roofline("config7", n, ek, ecnt["canon_bytes"] / LOG_STEPS), "counters": ecnt}
+    if n < LOG_SAME_TOTAL // LOG_STEPS:
+        # (the same total instances per measurement as the 2^22 line, so that
+        # its one exposed tail weighs the same: steady-state calls of n)
+        k = LOG_SAME_TOTAL // n
+        ts, _, tcnt = run_workload(GpuLeg(cfg, n, 0, 1, stream, dev, streams=LOG_STREAMS), n, k, 1, 1)
+        line["same_total"] = {"steps": k, "instances_per_s": tcnt["instances"] / ts}
     if general:
         with pxb.hooks(PXB_NO_EV="1"):
             gs, gk, gcnt = run_workload(GpuLeg(cfg, n, 0, 1, stream, dev, streams=LOG_STREAMS), n, LOG_STEPS, 1, 1)
