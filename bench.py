@@ -41,7 +41,16 @@ sys.path.insert(0, os.path.join(ROOT, "cloud-haskell-paxos_amd"))
 # after the other; workloads on one stream are unaffected.  Raised before
 # anything initialises HIP (torch is imported lazily), never lowered.
 HW_QUEUES = 16
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < HW_QUEUES:
+
+
+def _hw_queues():
+    try:
+        return int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+    except ValueError:
+        return 4
+
+
+if _hw_queues() < HW_QUEUES:
     os.environ["GPU_MAX_HW_QUEUES"] = str(HW_QUEUES)
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
@@ -459,7 +468,7 @@ def log_faulty_line(stream, dev, n=1 << 22, general=True):
     e2s, _, e2cnt = run_workload(GpuLeg(cfg, n, 0, 1, stream, dev), n, 2, 1, 1)
     line = {"workload": "faulty log mode: P=2, N=5, 10% loss, delay [1,4], crash windows, 16 Ticks / 8 steps",
             "instances_per_step": n, "steps": LOG_STEPS, "step_streams": LOG_STREAMS,
-            "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
+            "hw_queues": _hw_queues(),
             "instances_per_s": ecnt["instances"] / es,
             "commands_committed_per_s": ecnt["executes"] / es, "kernel_ms": ek,
             "instances_per_s_2_steps": e2cnt["instances"] / e2s,     # (2 steps on 2 streams: round 5's measurement)
